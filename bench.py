@@ -1,0 +1,273 @@
+#!/usr/bin/env python
+"""bench.py -- throughput of the stereo matching hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload north_star|cones|cv]
+                    [--mode pairdp|dshard] [--no-cpu-baseline]
+
+A step = one stereo pair through the hot path with inputs resident in HBM:
+u8 images -> z-norm + pad -> MC-CNN-fast tower (5 fp32-MFMA conv layers) on both
+images -> fused exact cost volume + WTA over D disparities -> float32 disparity.
+Default workload: the north-star size 1024x1024, D = 192 (BASELINE.json).
+
+N > 1 (one process per GPU under torchrun, RCCL):
+  pairdp : every rank matches its own pair each step (config 4) -- weak scaling,
+           no collective on the data path;
+  dshard : one pair per step, disparity-sharded over the ranks with the feature
+           row-band all-gather and the (min, argmin) all-gather (config 5) --
+           strong scaling.
+
+Rank 0 prints ONE JSON line.  `value` = H*W*D voxels of all pairs of all ranks /
+the max-over-ranks wall time of the K timed steps (Mpixel-disparities/s).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from scenedepthestimation_amd import ops  # noqa: E402
+from scenedepthestimation_amd.parallel import DisparityShardedMatcher, init_from_env  # noqa: E402
+from scenedepthestimation_amd.pipeline import StereoMatcher  # noqa: E402
+from scenedepthestimation_amd.synthetic import stereo_pair  # noqa: E402
+
+WORKLOADS = {
+    # name: (H, W, D, what)
+    "north_star": (1024, 1024, 192, "tower+cv_wta"),
+    "cones": (375, 450, 64, "tower+cv_wta"),
+    "cv": (1024, 1024, 192, "cv_wta"),
+}
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
+PEAK_VALU_F32_TOPS = 78.6     # non-fused f32 ops/s (one op per lane-slot; FMA counts 2 in the 157.3)
+NF = 64
+NLAYERS = 5
+
+
+def conv_flops(hout, wout):
+    return 2.0 * hout * wout * NF * 9 * NF
+
+
+class Timer:
+    """HIP events on torch's current stream (the stream every libsde launch uses)."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, e0):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.pairs.append((e0, e1))
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        if not self.pairs:
+            return float("nan")
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs]))
+
+    def reset(self):
+        self.pairs = []
+
+
+def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: Timer):
+    """One pass of the hot path, launched layer by layer so single kernels can be timed."""
+    L = m.nlayers
+    H, W = m.H, m.W
+    # activation ping-pong buffers for layers 3..L (layer 2 output is (H+2(L-2)) x ...)
+    acts = [torch.empty((H + 2 * (L - 2), W + 2 * (L - 2), NF), dtype=torch.float32, device=m.device)
+            for _ in range(2)]
+
+    def tower(i, timed):
+        e_t = t_tower.start() if timed else None
+        ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
+        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i])
+        hin, win = H + 2 * L - 4, W + 2 * L - 4
+        cur = 0
+        for layer in range(3, L + 1):
+            if layer == L:
+                o = m.feat[i]
+            else:   # a contiguous prefix of the ping-pong buffer, viewed at this layer's size
+                o = acts[cur ^ 1].view(-1)[: (hin - 2) * (win - 2) * NF].view(hin - 2, win - 2, NF)
+            src = acts[cur].view(-1)[: hin * win * NF].view(hin, win, NF)
+            e = t_conv.start() if (timed and layer == 3) else None
+            ops.tower_layer(src, m.packed, L, layer, o)
+            if e is not None:
+                t_conv.stop(e)
+            hin, win = hin - 2, win - 2
+            cur ^= 1
+        if e_t is not None:
+            t_tower.stop(e_t)
+
+    def step(timed=False):
+        if what == "tower+cv_wta":
+            tower(0, timed)
+            tower(1, timed)
+        e = t_cv.start() if timed else None
+        m.cost_wta()
+        if e is not None:
+            t_cv.stop(e)
+        return m.disp
+
+    return step
+
+
+def cpu_baseline(H, W, D, what, budget_s=15.0):
+    """The C oracle (single thread, exact) on a bounded row band of the same workload."""
+    import oracle
+    from scenedepthestimation_amd import mc_cnn
+    oracle.build()
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    w = mc_cnn.synthetic_weights(NLAYERS)
+    hw, hb = mc_cnn.layer_lists(w, NLAYERS)
+
+    def run(rows):
+        t0 = time.perf_counter()
+        if what == "tower+cv_wta":
+            feats = []
+            for img in (left, right):
+                pad = oracle.pad_image(oracle.znorm(img.astype(np.float32)), 2 * NLAYERS + 1)
+                feats.append(oracle.tower_forward(pad[:rows + 2 * NLAYERS], hw, hb))
+            fl, fr = feats
+        else:
+            from scenedepthestimation_amd.synthetic import features
+            fl, fr = features(rows, W, seed=0), features(rows, W, seed=1)
+            t0 = time.perf_counter()
+        oracle.cv_wta_shard(fl, fr, 0, D)
+        return time.perf_counter() - t0
+
+    t1 = run(1)
+    rows = int(max(1, min(H, budget_s / max(t1, 1e-6))))
+    t = run(rows)
+    return {"value": rows * W * D / t / 1e6, "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} of {H} rows x {W} cols x D={D} ({what}, exact C restatement, "
+                      f"{'fp64 tower + ' if what == 'tower+cv_wta' else ''}pairwise-f32 cost + WTA1), {t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
+    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    H, W, D, what = WORKLOADS[args.workload]
+    left, right, _ = stereo_pair(H, W, D, seed=rank)
+
+    t_conv, t_cv, t_tower = Timer(), Timer(), Timer()
+    if args.mode == "dshard" and world > 1:
+        dm = DisparityShardedMatcher(H, W, D, rank, world)
+        dm.m.load_images(left, right)
+
+        def step(timed=False):
+            e = t_tower.start() if timed else None
+            r = dm.match()
+            if e is not None:
+                t_tower.stop(e)
+            return r
+        pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
+    else:
+        m = StereoMatcher(H, W, D)
+        m.load_images(left, right)
+        if what == "cv_wta":
+            m.features()
+        step = make_step(m, what, t_conv, t_cv, t_tower)
+        pairs_per_step, scaling, par = world, "weak", f"pairdp{world}"
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+
+    vox = float(H) * W * D
+    value = vox * pairs_per_step * args.steps / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
+
+    roof = None
+    stages = {}
+    if args.mode == "pairdp" or world == 1:
+        cv_ms = t_cv.mean_ms()
+        bytes_cv = 4.0 * H * W * 2 * NF + 4.0 * H * W
+        stages["cv_wta_ms"] = cv_ms
+        stages["cv_wta_hbm_GBs"] = bytes_cv / (cv_ms * 1e-3) / 1e9
+        stages["cv_wta_valu_Tops"] = 127.0 * vox / (cv_ms * 1e-3) / 1e12
+        stages["cv_wta_valu_frac"] = stages["cv_wta_valu_Tops"] / PEAK_VALU_F32_TOPS
+        stages["cv_wta_Mvox_s"] = vox / (cv_ms * 1e-3) / 1e6
+        if what == "tower+cv_wta":
+            conv_ms = t_conv.mean_ms()
+            hout = H + 2 * (NLAYERS - 3)
+            wout = W + 2 * (NLAYERS - 3)
+            fl = conv_flops(hout, wout)
+            ach = fl / (conv_ms * 1e-3) / 1e12
+            stages["tower_ms_per_image"] = t_tower.mean_ms()
+            stages["conv_layer3_ms"] = conv_ms
+            roof = {"kernel": "conv64_mfma_kernel<false,false> (tower layer 3)", "bound": "mfma",
+                    "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+                    "traffic": None,
+                    "per_launch": f"{fl / 1e9:.2f} GFLOP = 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
+        else:
+            ach = bytes_cv / (cv_ms * 1e-3) / 1e9
+            roof = {"kernel": "cv64_kernel<LEFT,WTA> (fused exact cost volume + WTA)", "bound": "hbm",
+                    "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                    "traffic": None,
+                    "per_launch": f"{bytes_cv / 1e6:.1f} MB = 4*H*W*(2*64+1) over {cv_ms:.3f} ms; "
+                                  f"VALU {stages['cv_wta_valu_frac']:.2f} of {PEAK_VALU_F32_TOPS} Top/s"}
+    else:
+        stages["dshard_step_ms"] = t_tower.mean_ms()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(H, W, D, what)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpixel-disparities/sec (H*W*D cost voxels per second, end-to-end per pair)",
+            "value": value, "unit": "Mpixel-disparities/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "ms_per_pair": ms_step / pairs_per_step * world
+            if scaling == "weak" else ms_step,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded textured pair, band disparity field; synthetic He-normal tower weights)",
+            "config": {"workload": args.workload, "H": H, "W": W, "D": D, "C": NF, "nlayers": NLAYERS,
+                       "pipeline": what, "global_batch": pairs_per_step, "parallelism": par},
+            "roofline": roof, "cpu_baseline": cpu, "stages": stages,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

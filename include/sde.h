@@ -1,0 +1,178 @@
+/*
+ * sde.h -- C ABI of the MI355X-native stereo matching path (libsde.so).
+ *
+ * Drop-in boundary for WHDY/SceneDepthEstimation's matching path.  The
+ * reference's boundary is the Python function API of process_functional.py
+ * (star-imported by match_single.py:9 / match.py:10); each entry point below
+ * names the reference function or Numba kernel it replaces (file:line).
+ *
+ * Conventions
+ *   - every pointer argument except host-side helpers is a DEVICE pointer owned
+ *     by the caller; nothing here allocates, frees or synchronises, so every call
+ *     is stream-ordered and capturable into a hipGraph;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream);
+ *   - feature maps are [H][W][C] float32 (channels-last, the layout
+ *     compute_feature returns, process_functional.py:42-43);
+ *   - return value: SDE_OK or a negative sde_status; errors are detected before
+ *     any launch (argument checks) or right after it (hipGetLastError).
+ *   - reentrant: no global state besides the HIP module the loader registers.
+ */
+#ifndef SDE_H
+#define SDE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDE_ABI_VERSION 1
+
+typedef enum {
+    SDE_OK = 0,
+    SDE_ERR_ARG = -1,         /* bad size / null pointer / unsupported combination */
+    SDE_ERR_LAUNCH = -2,      /* hipGetLastError() after a launch */
+    SDE_ERR_WORKSPACE = -3,   /* workspace too small */
+} sde_status;
+
+typedef enum {
+    SDE_LAYOUT_DHW = 0,   /* [D][H][W]: compute_cost_volume / WTA1 (process_functional.py:48,96) */
+    SDE_LAYOUT_HWD = 1,   /* [H][W][D]: WTA and the GPU path (process_functional.py:76,120)      */
+} sde_layout;
+
+typedef enum {
+    SDE_WTA_INIT_INF = 0, /* best=+inf, `v < best`; no winner -> -1 (WTA/WTA1, :83-110)             */
+    SDE_WTA_INIT_D0 = 1,  /* best=v[0], `best > v` (WTA_and_SupixelRefinement_kernel, :805-811)      */
+} sde_wta_rule;
+
+typedef enum {
+    SDE_SIDE_LEFT = 1,    /* L[y][x][d]   = cost(x, d)        (process_functional.py:130) */
+    SDE_SIDE_RIGHT = 2,   /* R[y][x-d][d] = cost(x, d)        (process_functional.py:131) */
+} sde_side;
+
+/* ABI version (SDE_ABI_VERSION) and a static status string. */
+int sde_abi_version(void);
+const char *sde_status_string(int status);
+
+/*
+ * Cost volume, exact CPU-path numerics: cost(x,d) = -(0.0f + pairwise_sum_c
+ * fl[y][x][c]*fr[y][x-d][c]) with NumPy's float32 pairwise order (no FMA).
+ *   layout = SDE_LAYOUT_DHW, sides = LEFT, invalid = -0.0f
+ *       replaces compute_cost_volume (process_functional.py:48-73), bit-exact;
+ *   layout = SDE_LAYOUT_HWD, sides = LEFT|RIGHT, invalid = 1.0f
+ *       replaces compute_cost_volume_kernel (process_functional.py:120-131)
+ *       including its never-written voxels (:1111-1114).
+ * out_left / out_right: D*H*W floats each (the one not requested may be NULL).
+ */
+int sde_cost_volume(const float *fl, const float *fr, int H, int W, int C, int D, int layout,
+                    int sides, float invalid, float *out_left, float *out_right, void *stream);
+
+/*
+ * First-minimum over d of an existing volume -> disparity as float32.
+ * Replaces WTA1 (process_functional.py:96-113, DHW), WTA (:76-93, HWD) and
+ * WTA_and_SupixelRefinement_kernel (:800-837, HWD + SDE_WTA_INIT_D0).
+ * A pixel without a winner (all NaN / +inf under INIT_INF) gets -1.0f; the
+ * reference asserts there (:89,109) and the Python layer raises.
+ */
+int sde_wta(const float *vol, int H, int W, int D, int layout, int rule, float *disp, void *stream);
+
+/*
+ * Fused cost volume + WTA over the disparity shard [d0, d1) without
+ * materialising the volume: WTA1(compute_cost_volume(fl, fr, D)) bit-exact when
+ * d0 = 0, d1 = D.  Outputs (each optional, NULL to skip): disp (float32 argmin),
+ * min_cost (float32 first-min value) and argmin (int32, -1 if none), [H][W].
+ * Shards merge bit-exactly with sde_argmin_merge (ties -> lower d).
+ */
+int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, int d1, float *disp,
+               float *min_cost, int32_t *argmin, void *stream);
+
+/*
+ * Ordered merge of per-shard (min, argmin) pairs: shard s covers a disparity
+ * range that precedes shard s+1's; strict `<` keeps the earliest on ties.
+ * mins/args: [nshards][npix].  disp: float32 [npix].
+ */
+int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_t npix, float *disp,
+                     void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* MC-CNN-fast branch (mc_cnn_brunch.py:31-48; compute_feature's sess.run,   */
+/* process_functional.py:11-45).  nlayers 3x3 VALID convs, nf = 64 maps.     */
+/* ---------------------------------------------------------------------- */
+
+/* Number of floats of the packed (device-layout) weight blob. */
+int64_t sde_tower_packed_floats(int nlayers, int nf);
+
+/*
+ * HOST helper: pack TF HWIO weights ([3][3][Cin][nf], `conv{k}/weights:0`) and
+ * biases ([nf], `conv{k}/biases:0`) of nlayers layers into `packed` (host memory,
+ * sde_tower_packed_floats() floats).  Copy the blob to the device once.
+ */
+int sde_tower_pack_weights(const float *const *hwio, const float *const *biases, int nlayers, int nf,
+                           float *packed);
+
+/* Device workspace bytes needed by sde_tower_forward for an H x W output. */
+int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf);
+
+/*
+ * img_pad: float32 [(H+2*nlayers)][(W+2*nlayers)] zero-padded normalised image
+ * (process_functional.py:13-19).  feat: float32 [H][W][nf], L2-normalised per
+ * pixel (mc_cnn_brunch.py:48).  packed: device copy of the packed weights.
+ */
+int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
+                      float *feat, void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
+ * One layer of the tower as a single kernel launch (for per-layer timing and
+ * pipelining): layer == 2 -> conv1+conv2 fused, `in` = padded image Hin x Win
+ * floats, out (Hin-4) x (Win-4) x nf; layer in 3..nlayers -> `in` = Hin x Win x
+ * nf activations, out (Hin-2) x (Win-2) x nf.  Layer nlayers L2-normalises.
+ */
+int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
+                    float *out, void *stream);
+
+/*
+ * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):
+ * u8 image -> (I - mean) / std (population std, float32) written into the
+ * interior of the zero-padded buffer out_pad [(H+2*pad)][(W+2*pad)].
+ * stats: 2 floats of device scratch (mean, std) written by the call.
+ */
+int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, float *stats,
+                      void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Semi-global matching (GPU path of disparity_compute_by_gpu,               */
+/* process_functional.py:1093-1267).                                         */
+/* ---------------------------------------------------------------------- */
+
+/* sgm_penelty_kernel (process_functional.py:134-262): pen [H][W][16] float32. */
+int sde_sgm_penalties(const uint8_t *img, int H, int W, double P1, double P2, int64_t threshold,
+                      double lambda, float *pen, void *stream);
+
+/*
+ * 8-path SGM for one side (SGM_*_kernel, process_functional.py:265-797, launch
+ * order :1166-1203): S [H][W][D] += path costs, direction order UD, DU, LR, RL,
+ * UD-LR, DU-LR, UD-RL, DU-RL; fp64 recurrence, float32 S.  The caller zeroes S
+ * (the reference uploads np.zeros, :1116-1119).  cv: [H][W][D] with invalid
+ * voxels = 1.0 (sde_cost_volume HWD).  Requires H >= 2, W >= 2.
+ */
+int sde_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float *S, void *stream);
+
+/* One direction (0..7 in the order above) of sde_sgm_8path. */
+int sde_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int direction, float *S,
+                      void *stream);
+
+/* is_error_match_kernel (process_functional.py:977-1000): lrc_l/lrc_r u8 [H][W], caller-zeroed. */
+int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,
+                 void *stream);
+
+/* LRC_kernel left output (process_functional.py:1003-1088). */
+int sde_lrc_fill(const float *disp_l, const uint8_t *lrc_l, int H, int W, float *out, void *stream);
+
+/* Median_Filter_kernel (process_functional.py:840-879): 5x5 median of src into the interior of dst. */
+int sde_median5(const float *src, int H, int W, float *dst, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDE_H */

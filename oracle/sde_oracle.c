@@ -1,0 +1,452 @@
+/*
+ * sde_oracle.c -- CPU restatement of the WHDY/SceneDepthEstimation matching path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product path (scenedepthestimation_amd/) never links or calls it.
+ *
+ * Parity status
+ *   - cost volume / WTA / WTA1: PINNED against golden vectors produced by the
+ *     reference's own NumPy functions (tests/golden/make_golden.py executes
+ *     process_functional.py:48-113 extracted with `ast`).
+ *   - SGM penalties / 8-path SGM / LR check / LRC fill / median / tower:
+ *     PARITY UNPINNED -- the reference implements them as Numba CUDA kernels
+ *     and a TF1 graph, neither runnable here.  They are restated line-by-line
+ *     from the reference source (citations below) and cross-checked against an
+ *     independent literal Python restatement in tests/ (small sizes).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA contraction, the
+ * reference's NumPy products and sums are separately rounded).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* NumPy float32 add.reduce: result = 0.0f + pairwise_sum(a, n).             */
+/* numpy/_core/src/umath/loops_utils.h.src (pairwise_sum, PW_BLOCKSIZE 128); */
+/* the leading 0.0f is add's reduction identity (turns a -0.0 sum into +0).  */
+/* ------------------------------------------------------------------------ */
+static float pw_sum_strided(const float *a, long n, long stride)
+{
+    if (n < 8) {
+        float res = 0.0f;
+        for (long i = 0; i < n; i++) res += a[i * stride];
+        return res;
+    } else if (n <= 128) {
+        float r[8];
+        for (int j = 0; j < 8; j++) r[j] = a[j * stride];
+        long i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += a[(i + j) * stride];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += a[i * stride];
+        return res;
+    } else {
+        long n2 = n / 2;
+        n2 -= n2 % 8;
+        return pw_sum_strided(a, n2, stride) + pw_sum_strided(a + n2 * stride, n - n2, stride);
+    }
+}
+
+EXPORT float sdeo_np_sum_f32(const float *a, long n)
+{
+    return 0.0f + pw_sum_strided(a, n, 1);
+}
+
+/* -(np.sum(np.multiply(l, r))) for one voxel: process_functional.py:58,72 */
+static float np_neg_dot(const float *l, const float *r, int C, float *tmp)
+{
+    for (int c = 0; c < C; c++) tmp[c] = l[c] * r[c];
+    float s = 0.0f + pw_sum_strided(tmp, C, 1);
+    return -1.0f * s;   /* `-1 * left_cost_volume` (process_functional.py:72) */
+}
+
+/*
+ * compute_cost_volume (process_functional.py:48-73): out[d][y][x] =
+ * -(sum_c fl[y][x][c] * fr[y][x-d][c]) for x >= d, -0.0 otherwise.
+ */
+EXPORT void sdeo_cost_volume_dhw(const float *fl, const float *fr, int H, int W, int C, int D,
+                                 float *out)
+{
+    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+    for (int d = 0; d < D; d++)
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) {
+                float *o = out + ((size_t)d * H + y) * W + x;
+                if (x >= d)
+                    *o = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
+                else
+                    *o = -0.0f;   /* np.zeros then `-1 *` */
+            }
+    free(tmp);
+}
+
+/*
+ * GPU-path volume layout [H][W][D] (process_functional.py:120-131): left
+ * L[y][x][d] = cost(x,d) for x >= d; right R[y][x-d][d] = cost(x,d); every
+ * voxel never written keeps `invalid` (1.0 in the reference, :1111-1114).
+ * Valid costs use the CPU-path numerics above.
+ */
+EXPORT void sdeo_cost_volume_hwd(const float *fl, const float *fr, int H, int W, int C, int D,
+                                 float invalid, float *outl, float *outr)
+{
+    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+    size_t n = (size_t)H * W * D;
+    if (outl) for (size_t i = 0; i < n; i++) outl[i] = invalid;
+    if (outr) for (size_t i = 0; i < n; i++) outr[i] = invalid;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D && d <= x; d++) {
+                float c = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
+                if (outl) outl[((size_t)y * W + x) * D + d] = c;
+                if (outr) outr[((size_t)y * W + x - d) * D + d] = c;
+            }
+    free(tmp);
+}
+
+/* WTA1 (process_functional.py:96-113): first d with cost < running min (init +inf). */
+EXPORT int sdeo_wta1_dhw(const float *cv, int D, int H, int W, float *disp)
+{
+    int bad = 0;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float best = INFINITY;
+            int arg = -1;
+            for (int d = 0; d < D; d++) {
+                float v = cv[((size_t)d * H + y) * W + x];
+                if (v < best) { best = v; arg = d; }
+            }
+            if (arg < 0) bad++;
+            disp[(size_t)y * W + x] = (float)arg;
+        }
+    return bad;   /* reference asserts arg >= 0 (:109) */
+}
+
+/* WTA (process_functional.py:76-93): same rule on an [H][W][D] volume. */
+EXPORT int sdeo_wta_hwd(const float *cv, int H, int W, int D, float *disp)
+{
+    int bad = 0;
+    for (size_t p = 0; p < (size_t)H * W; p++) {
+        float best = INFINITY;
+        int arg = -1;
+        for (int d = 0; d < D; d++) {
+            float v = cv[p * D + d];
+            if (v < best) { best = v; arg = d; }
+        }
+        if (arg < 0) bad++;
+        disp[p] = (float)arg;
+    }
+    return bad;
+}
+
+/*
+ * WTA_and_SupixelRefinement_kernel (process_functional.py:800-837): first-min
+ * with `min_s > tmp`, initialised from d = 0 (not +inf).
+ */
+EXPORT void sdeo_wta_sgm_hwd(const float *S, int H, int W, int D, float *disp)
+{
+    for (size_t p = 0; p < (size_t)H * W; p++) {
+        float m = S[p * D];
+        int arg = 0;
+        for (int d = 1; d < D; d++) {
+            float v = S[p * D + d];
+            if (m > v) { m = v; arg = d; }
+        }
+        disp[p] = (float)arg;
+    }
+}
+
+/*
+ * Fused cost volume + first-min over a disparity shard [d0, d1) without
+ * materialising the volume: min value and argmin (global d index, -1 if no
+ * candidate beat +inf).  Invalid voxels (x < d) take -0.0 as in the CPU path.
+ */
+EXPORT void sdeo_cv_wta_shard(const float *fl, const float *fr, int H, int W, int C, int d0, int d1,
+                              float *minv, int32_t *argmin)
+{
+    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float best = INFINITY;
+            int arg = -1;
+            for (int d = d0; d < d1; d++) {
+                float v = (x >= d) ? np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp)
+                                   : -0.0f;
+                if (v < best) { best = v; arg = d; }
+            }
+            minv[(size_t)y * W + x] = best;
+            argmin[(size_t)y * W + x] = arg;
+        }
+    free(tmp);
+}
+
+/* ------------------------------------------------------------------------ */
+/* SGM penalties: sgm_penelty_kernel (process_functional.py:134-262).        */
+/* Numba types uint8 - uint8 as uint64 (wraps), `-diff if diff < 0` is a     */
+/* no-op, and `diff > threshold` compares as float64: reduced iff            */
+/* nb < c or nb > c + thr.  The (y-1) block writes ch 2/3 but the (y+1)      */
+/* block (:159-172) overwrites them, so ch 0/1 stay 0.                       */
+/* ------------------------------------------------------------------------ */
+EXPORT void sdeo_sgm_penalties(const uint8_t *img, int H, int W, double P1, double P2, long thr,
+                               double lambda, float *pen)
+{
+    const float fP1 = (float)P1, fP2 = (float)P2;
+    const float rP1 = (float)(P1 / lambda), rP2 = (float)(P2 / lambda);
+    static const int nb[8][3] = {
+        /* dy, dx, channel */
+        {-1, 0, 2}, {+1, 0, 2}, {0, -1, 4}, {0, +1, 6},
+        {+1, -1, 8}, {+1, +1, 10}, {-1, +1, 12}, {-1, -1, 14},
+    };
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            float *p = pen + ((size_t)y * W + x) * 16;
+            p[0] = 0.0f;
+            p[1] = 0.0f;
+            const uint64_t c = img[(size_t)y * W + x];
+            for (int k = 0; k < 8; k++) {
+                int yy = y + nb[k][0], xx = x + nb[k][1], ch = nb[k][2];
+                if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+                    uint64_t diff = (uint64_t)img[(size_t)yy * W + xx] - c;
+                    int red = (double)diff > (double)thr;
+                    p[ch] = red ? rP1 : fP1;
+                    p[ch + 1] = red ? rP2 : fP2;
+                } else {
+                    p[ch] = fP1;
+                    p[ch + 1] = fP2;
+                }
+            }
+        }
+}
+
+/* ------------------------------------------------------------------------ */
+/* 8-path SGM (process_functional.py:265-797, launch order :1166-1203).      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double *L;      /* path cost of the previous pixel, fp64 (Numba-unified) */
+    double *Ln;
+    double m, mP2;
+} sgm_state;
+
+/* One SGM_Interation (:265-343) at pixel (r,c). */
+static void sgm_step(const float *C, float *S, sgm_state *st, int D, int restart, double P1, double P2,
+                     int calc_min)
+{
+    double *L = st->L, *Ln = st->Ln;
+    if (restart) {
+        for (int d = 0; d < D; d++) Ln[d] = (double)C[d];
+    } else {
+        for (int d = 0; d < D; d++) {
+            double b = L[d];
+            if (d > 0) { double t = L[d - 1] + P1; if (t < b) b = t; }
+            if (d < D - 1) { double t = L[d + 1] + P1; if (t < b) b = t; }
+            if (st->mP2 < b) b = st->mP2;
+            Ln[d] = (double)C[d] + (b - st->m);
+        }
+    }
+    for (int d = 0; d < D; d++) S[d] = (float)((double)S[d] + Ln[d]);
+    if (calc_min) {
+        double m = Ln[0];
+        for (int d = 1; d < D; d++) if (Ln[d] < m) m = Ln[d];
+        st->m = m;
+        st->mP2 = m + P2;
+    }
+    st->L = Ln;
+    st->Ln = L;
+}
+
+static inline int sgm_nsteps(int n) { return n - 1 > 2 ? n - 1 : 2; }
+
+enum { SGM_UD = 0, SGM_DU, SGM_LR, SGM_RL, SGM_UDLR, SGM_DULR, SGM_UDRL, SGM_DURL };
+
+/* One direction over one side: cv/pen/S are [H][W][D], [H][W][16], [H][W][D]. */
+EXPORT void sdeo_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int dir,
+                               float *S)
+{
+    double *b0 = (double *)malloc(sizeof(double) * D), *b1 = (double *)malloc(sizeof(double) * D);
+#define CV(r, c) (cv + ((size_t)(r) * W + (c)) * D)
+#define SS(r, c) (S + ((size_t)(r) * W + (c)) * D)
+#define PEN(r, c, ch) ((double)pen[((size_t)(r) * W + (c)) * 16 + (ch)])
+    if (dir == SGM_UD || dir == SGM_DU) {
+        int n = sgm_nsteps(H);
+        for (int c = 0; c < W; c++) {
+            sgm_state st = {b0, b1, 1.0, 1.0};
+            for (int k = 0; k < n; k++) {
+                int r = dir == SGM_UD ? k : H - 1 - k;
+                double P1 = 0.0, P2;
+                if (dir == SGM_UD) { if (r - 1 >= 0) P1 = PEN(r - 1, c, 2); P2 = PEN(r, c, 3); }
+                else               { if (r + 1 < H)  P1 = PEN(r + 1, c, 0); P2 = PEN(r, c, 1); }
+                sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
+            }
+        }
+    } else if (dir == SGM_LR || dir == SGM_RL) {
+        int n = sgm_nsteps(W);
+        for (int r = 0; r < H; r++) {
+            sgm_state st = {b0, b1, 1.0, 1.0};
+            for (int k = 0; k < n; k++) {
+                int c = dir == SGM_LR ? k : W - 1 - k;
+                double P1 = 0.0, P2;
+                if (dir == SGM_LR) { if (c - 1 >= 0) P1 = PEN(r, c - 1, 6); P2 = PEN(r, c, 7); }
+                else               { if (c + 1 < W)  P1 = PEN(r, c + 1, 4); P2 = PEN(r, c, 5); }
+                sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
+            }
+        }
+    } else {
+        int n = sgm_nsteps(H);
+        int down = (dir == SGM_UDLR || dir == SGM_UDRL);
+        int right = (dir == SGM_UDLR || dir == SGM_DULR);
+        int p1ch = dir == SGM_UDLR ? 10 : dir == SGM_DULR ? 12 : dir == SGM_UDRL ? 8 : 14;
+        for (int c0 = 0; c0 < W; c0++) {
+            sgm_state st = {b0, b1, 1.0, 1.0};
+            int c = c0;
+            for (int k = 0; k < n; k++) {
+                int r = down ? k : H - 1 - k;
+                int restart = (k == 0);
+                if (k > 0) {
+                    c += right ? 1 : -1;
+                    if (right && c >= W) { c = 0; restart = 1; }
+                    if (!right && c < 0) { c = W - 1; restart = 1; }
+                }
+                int pr = down ? r - 1 : r + 1;
+                int pc = right ? c - 1 : c + 1;
+                double P1 = 0.0;
+                if (pr >= 0 && pr < H && pc >= 0 && pc < W) P1 = PEN(pr, pc, p1ch);
+                double P2 = PEN(r, c, p1ch + 1);
+                sgm_step(CV(r, c), SS(r, c), &st, D, restart, P1, P2, k < n - 1);
+            }
+        }
+    }
+#undef CV
+#undef SS
+#undef PEN
+    free(b0);
+    free(b1);
+}
+
+/* All 8 directions in the reference launch order; S is accumulated (caller zeroes it). */
+EXPORT void sdeo_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float *S)
+{
+    for (int dir = 0; dir < 8; dir++) sdeo_sgm_direction(cv, pen, H, W, D, dir, S);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Post-processing ("next" rows): is_error_match_kernel (:977-1000),        */
+/* LRC_kernel (:1003-1088), Median_Filter_kernel (:840-879).                 */
+/* uint8() index casts are restated as truncation toward zero then mod 256  */
+/* (PARITY UNPINNED: Numba's float->uint8 out-of-range behaviour).           */
+/* ------------------------------------------------------------------------ */
+static inline int u8cast(double v) { long long t = (long long)v; return (int)(t & 255); }
+
+EXPORT void sdeo_lr_check(const float *dl, const float *dr, int H, int W, uint8_t *lrcl, uint8_t *lrcr)
+{
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            double ld = dl[(size_t)y * W + x];
+            double rd = (double)x - ld;
+            if (rd >= 0) {
+                double r2 = dr[(size_t)y * W + u8cast(rd)];
+                double mn = ld - r2;
+                lrcl[(size_t)y * W + x] = (mn > 1 || mn < -1) ? 1 : 0;
+            }
+            double rd2 = dr[(size_t)y * W + x];
+            double ld2 = (double)x + rd2;
+            if (ld2 < W) {
+                double l2 = dl[(size_t)y * W + u8cast(ld2)];
+                double mn = rd2 - l2;
+                lrcr[(size_t)y * W + x] = (mn > 1 || mn < -1) ? 1 : 0;
+            }
+        }
+}
+
+EXPORT void sdeo_lrc_fill(const float *dl, const uint8_t *lrcl, int H, int W, float *out)
+{
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            size_t p = (size_t)y * W + x;
+            if (lrcl[p] == 1) {
+                int number = 0;
+                double sum = 0.0;   /* int 0 + float32 -> float64 in Numba */
+                int iy = y;
+                while (iy >= 0 && lrcl[(size_t)iy * W + x] == 1) iy--;
+                if (iy >= 0) { number++; sum += dl[(size_t)iy * W + x]; }
+                iy = y;
+                while (iy < H && lrcl[(size_t)iy * W + x] == 1) iy++;
+                if (iy < H) { number++; sum += dl[(size_t)iy * W + x]; }
+                int ix = x;
+                while (ix < W && lrcl[(size_t)y * W + ix] == 1) ix++;
+                if (ix < W) { number++; sum += dl[(size_t)y * W + ix]; }
+                ix = x;
+                while (ix >= 0 && lrcl[(size_t)y * W + ix] == 1) ix--;
+                if (ix >= 0) { number++; sum += dl[(size_t)y * W + ix]; }
+                out[p] = number > 0 ? (float)(sum / number) : dl[p];
+            } else {
+                out[p] = dl[p];
+            }
+        }
+}
+
+/* 5x5 median of the interior (2-px border of `out` untouched): partial selection sort to the 13th. */
+EXPORT void sdeo_median5(const float *in, int H, int W, float *out)
+{
+    for (int y = 2; y + 2 < H; y++)
+        for (int x = 2; x + 2 < W; x++) {
+            float w[25];
+            for (int i = -2; i <= 2; i++)
+                for (int j = -2; j <= 2; j++) w[(i + 2) * 5 + j + 2] = in[(size_t)(y + i) * W + x + j];
+            float cur = 0.0f;
+            for (int i = 0; i < 13; i++) {
+                cur = w[i];
+                int ci = i;
+                for (int j = i + 1; j < 25; j++)
+                    if (cur > w[j]) { cur = w[j]; ci = j; }
+                w[ci] = w[i];
+            }
+            out[(size_t)y * W + x] = cur;
+        }
+}
+
+/* ------------------------------------------------------------------------ */
+/* MC-CNN-fast branch (mc_cnn_brunch.py:31-48,70-92) in fp64: 3x3 VALID      */
+/* cross-correlation, HWIO weights, bias, ReLU on all but the last layer,    */
+/* then tf.nn.l2_normalize(dim=-1) = x * rsqrt(max(sum x^2, 1e-12)).         */
+/* ------------------------------------------------------------------------ */
+EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers, int nf,
+                               const float *const *weights, const float *const *biases, float *out)
+{
+    int h = Hp, w = Wp, cin = 1;
+    double *cur = (double *)malloc(sizeof(double) * (size_t)Hp * Wp);
+    for (size_t i = 0; i < (size_t)Hp * Wp; i++) cur[i] = img_pad[i];
+    for (int l = 0; l < nlayers; l++) {
+        int ho = h - 2, wo = w - 2;
+        double *nxt = (double *)malloc(sizeof(double) * (size_t)ho * wo * nf);
+        const float *Wt = weights[l], *B = biases[l];
+        for (int y = 0; y < ho; y++)
+            for (int x = 0; x < wo; x++)
+                for (int n = 0; n < nf; n++) {
+                    double s = 0.0;
+                    for (int ky = 0; ky < 3; ky++)
+                        for (int kx = 0; kx < 3; kx++)
+                            for (int c = 0; c < cin; c++)
+                                s += cur[((size_t)(y + ky) * w + (x + kx)) * cin + c] *
+                                     (double)Wt[((ky * 3 + kx) * cin + c) * nf + n];
+                    s += B[n];
+                    if (l < nlayers - 1 && s < 0) s = 0;
+                    nxt[((size_t)y * wo + x) * nf + n] = s;
+                }
+        free(cur);
+        cur = nxt;
+        h = ho;
+        w = wo;
+        cin = nf;
+    }
+    for (size_t p = 0; p < (size_t)h * w; p++) {
+        double ss = 0.0;
+        for (int n = 0; n < nf; n++) ss += cur[p * nf + n] * cur[p * nf + n];
+        double inv = 1.0 / sqrt(ss > 1e-12 ? ss : 1e-12);
+        for (int n = 0; n < nf; n++) out[p * nf + n] = (float)(cur[p * nf + n] * inv);
+    }
+    free(cur);
+}

@@ -1,0 +1,93 @@
+"""ctypes binding of libsde.so (the C ABI declared in include/sde.h).
+
+torch is imported first on purpose: its bundled HIP runtime (SONAME
+libamdhip64.so.7) is then the one libsde.so binds to, so device pointers and
+streams handed over from torch are valid in our launches.
+
+There is no fallback: if the library is missing or does not export a symbol of
+include/sde.h, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (load torch's HIP runtime before libsde.so)
+
+from ._build import INCLUDE, LIB
+
+c_int, c_int64, c_float, c_double, c_void_p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+SDE_OK = 0
+SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
+SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
+SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
+
+# name -> (restype, argtypes); must cover every function declared in include/sde.h
+SIGNATURES = {
+    "sde_abi_version": (c_int, []),
+    "sde_status_string": (c_char_p, [c_int]),
+    "sde_cost_volume": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                c_void_p, c_void_p, c_void_p]),
+    "sde_wta": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_cv_wta": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
+    "sde_argmin_merge": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
+    "sde_tower_packed_floats": (c_int64, [c_int, c_int]),
+    "sde_tower_pack_weights": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int,
+                                       c_void_p]),
+    "sde_tower_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
+    "sde_tower_forward": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                  c_int64, c_void_p]),
+    "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
+                                  c_void_p]),
+    "sde_sgm_8path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_lr_check": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sde_lrc_fill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sde_median5": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+}
+
+
+def header_functions(path: str = os.path.join(INCLUDE, "sde.h")):
+    """Names of the functions declared in include/sde.h (parsed from the header text)."""
+    with open(path) as fh:
+        text = fh.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sde_[a-z0-9_]+)\s*\(", text)))
+
+
+class SdeError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB):
+        raise ImportError(f"{LIB} is missing: build it with `python -m scenedepthestimation_amd._build` "
+                          "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB)
+    missing = []
+    for name, (res, args) in SIGNATURES.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            missing.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    if missing:
+        raise ImportError(f"{LIB} does not export {missing}")
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, what: str):
+    if status != SDE_OK:
+        msg = lib.sde_status_string(status)
+        raise SdeError(f"{what} failed: {msg.decode() if msg else status} ({status})")

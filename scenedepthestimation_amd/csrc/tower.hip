@@ -1,0 +1,384 @@
+// tower.hip -- MC-CNN-fast Siamese branch on fp32 MFMA (gfx950).
+//
+// Replaces mc_cnn_brunch.py:31-48 (Net.construct) + :70-92 (conv) as run by
+// compute_feature (process_functional.py:21-39): nlayers x [3x3 VALID conv,
+// bias, ReLU] (no ReLU on the last), then tf.nn.l2_normalize over channels.
+//
+// Layers 2..n are an implicit GEMM on v_mfma_f32_32x32x2_f32 (exact f32 in /
+// f32 accumulate, the 157 TF fp32 matrix rate): out[n][pixel] = sum over
+// (tap, c) of W[tap][n][c] * in[pixel + tap][c].  A = weights (M = 64 output
+// maps = 2 tiles of 32), B = input pixels (N = 32 pixels of one output row),
+// K = 64 input maps per tap x 9 taps.
+//
+// Workgroup: 512 threads = 8 waves, output tile 8 rows x 32 columns, wave w
+// owns output row w (2 accumulators of 32x32).  LDS: the (8+2) x (32+2) x 64
+// input tile (87 KB) stays resident for all 9 taps; each tap's 64x64 weight
+// slice (16 KB) is double-buffered (prefetched into registers during the
+// previous tap's MFMAs).  Both LDS images are XOR-swizzled at 8-B granularity
+// (pair slot ^= row & 31) so the 32 lanes of a ds_read_b64 half hit 64
+// distinct banks.  Layer 1 (Cin = 1, 9 MACs per output) is computed on VALU
+// straight into layer 2's LDS input tile, so its output never touches HBM; the
+// last layer's epilogue L2-normalises each pixel (its 64 channels live in a
+// lane pair l, l^32) before the store.
+#include "sde_common.h"
+
+namespace sde {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int TW_TY = 8;                 // output rows per workgroup (one per wave)
+constexpr int TW_TX = 32;                // output cols per workgroup (MFMA N)
+constexpr int TW_IY = TW_TY + 2;         // input tile rows
+constexpr int TW_IX = TW_TX + 2;         // input tile cols
+constexpr int TW_NPIX = TW_IY * TW_IX;   // 340
+constexpr int NF = 64;                   // feature maps (the reference's num_of_conv_feature_maps)
+constexpr int L1_FLOATS = NF + 9 * NF;           // bias + [tap][n]
+constexpr int LK_FLOATS = NF + 9 * NF * NF;      // bias + [tap][n][c]
+
+// float2 slot of channel pair `pair` (0..31) of pixel/row `p` in a swizzled 64-float row
+__device__ __forceinline__ int pslot(int p, int pair) { return p * 32 + (pair ^ (p & 31)); }
+
+// write channels 4q..4q+3 of row p (a float4) into the swizzled image
+__device__ __forceinline__ void put4(float2 *img, int p, int q, float4 v)
+{
+    const int x = p & 31;
+    const int unit = q ^ (x >> 1);
+    float4 w = (x & 1) ? make_float4(v.z, v.w, v.x, v.y) : v;
+    *reinterpret_cast<float4 *>(img + p * 32 + 2 * unit) = w;
+}
+
+// Load the 64x64 weight slice of one tap into registers (16 KB / 512 threads = 2 float4).
+__device__ __forceinline__ void load_tap(const float *__restrict__ wk, int tap, float4 (&r)[2])
+{
+    const float4 *src = reinterpret_cast<const float4 *>(wk + (size_t)tap * NF * NF);
+#pragma unroll
+    for (int i = 0; i < 2; i++) r[i] = src[threadIdx.x + i * 512];
+}
+
+__device__ __forceinline__ void store_tap(float2 *wt, const float4 (&r)[2])
+{
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int idx = threadIdx.x + i * 512;   // float4 index: n = idx / 16, q = idx % 16
+        put4(wt, idx >> 4, idx & 15, r[i]);
+    }
+}
+
+// FIRST: the input tile is conv1 (Cin = 1) of the padded image, computed here.
+// LAST : no ReLU, L2-normalise over the 64 channels before the store.
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restrict__ in, int Hin, int Win,
+                                                          const float *__restrict__ w1blob,
+                                                          const float *__restrict__ wkblob,
+                                                          float *__restrict__ out, int Hout, int Wout)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 smem[];
+    float2 *tile = smem;                          // TW_NPIX rows x 32 pairs
+    float2 *wt0 = smem + TW_NPIX * 32;            // 64 rows x 32 pairs
+    float2 *wt1 = wt0 + NF * 32;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int tx0 = blockIdx.x * TW_TX;
+    const int ty0 = blockIdx.y * TW_TY;
+    const float *bias = wkblob;
+    const float *wk = wkblob + NF;
+
+    float4 wreg[2];
+    load_tap(wk, 0, wreg);
+
+    // ---- input tile -> LDS ------------------------------------------------
+    if (!FIRST) {
+        // Hin x Win x 64 activations; tile pixel (iy, ix) = in[ty0+iy][tx0+ix]
+        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
+            const int p = idx >> 4, q = idx & 15;
+            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (iy < Hin && ix < Win) v = reinterpret_cast<const float4 *>(in + ((size_t)iy * Win + ix) * NF)[q];
+            put4(tile, p, q, v);
+        }
+    } else {
+        // `in` is the padded image (Hin x Win floats); conv1 output has (Hin-2) x (Win-2)
+        // pixels.  Tile pixel (iy, ix) = relu(b1 + sum_tap img[ty0+iy+dy][tx0+ix+dx] * w1[tap][n]).
+        const float *b1 = w1blob;
+        const float *w1 = w1blob + NF;
+        const int H1 = Hin - 2, W1 = Win - 2;
+        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
+            const int p = idx >> 4, q = idx & 15;
+            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (iy < H1 && ix < W1) {
+                float im[9];
+#pragma unroll
+                for (int t = 0; t < 9; t++) im[t] = in[(size_t)(iy + t / 3) * Win + ix + t % 3];
+                float a[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int n = 4 * q + j;
+                    float s = 0.0f;
+#pragma unroll
+                    for (int t = 0; t < 9; t++) s = fmaf(im[t], w1[t * NF + n], s);
+                    s += b1[n];
+                    a[j] = s > 0.0f ? s : 0.0f;
+                }
+                v = make_float4(a[0], a[1], a[2], a[3]);
+            }
+            put4(tile, p, q, v);
+        }
+    }
+    store_tap(wt0, wreg);
+    __syncthreads();
+
+    // ---- 9 taps x 16 k-quads x (2 M-tiles x 2 k-steps) MFMAs ----------------
+    floatx16 acc0 = {0}, acc1 = {0};
+    const int j = lane & 31;        // output column within the tile (B col / A row)
+    const int h = lane >> 5;        // k half: channels 2h, 2h+1 of each k-quad
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap++) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        float2 *wt = (tap & 1) ? wt1 : wt0;
+        if (tap < 8) load_tap(wk, tap + 1, wreg);
+        const int p = (wave + ky) * TW_IX + (j + kx);
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const float2 b = tile[pslot(p, 2 * t + h)];
+            const float2 a0 = wt[pslot(j, 2 * t + h)];
+            const float2 a1 = wt[pslot(j + 32, 2 * t + h)];
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b.x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b.y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b.y, acc1, 0, 0, 0);
+        }
+        if (tap < 8) store_tap((tap & 1) ? wt0 : wt1, wreg);
+        __syncthreads();
+    }
+
+    // ---- epilogue: bias (+ReLU | L2-normalise), float4 stores ---------------
+    // lane holds pixel column j, channels n = mt*32 + 8g + 4h + e in acc_mt[4g + e]
+    float v[2][16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int n = 8 * (r >> 2) + 4 * h + (r & 3);
+        v[0][r] = acc0[r] + bias[n];
+        v[1][r] = acc1[r] + bias[32 + n];
+    }
+    if (!LAST) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            v[0][r] = v[0][r] > 0.0f ? v[0][r] : 0.0f;
+            v[1][r] = v[1][r] > 0.0f ? v[1][r] : 0.0f;
+        }
+    } else {
+        float ss = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; r++) ss += v[0][r] * v[0][r] + v[1][r] * v[1][r];
+        ss += __shfl_xor(ss, 32, 64);
+        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+#pragma unroll
+        for (int r = 0; r < 16; r++) { v[0][r] *= inv; v[1][r] *= inv; }
+    }
+    const int oy = ty0 + wave, ox = tx0 + j;
+    if (oy < Hout && ox < Wout) {
+        float *dst = out + ((size_t)oy * Wout + ox) * NF;
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+                *reinterpret_cast<float4 *>(dst + mt * 32 + 8 * g + 4 * h) =
+                    make_float4(v[mt][4 * g], v[mt][4 * g + 1], v[mt][4 * g + 2], v[mt][4 * g + 3]);
+    }
+}
+
+// nlayers == 1: conv1 + L2 normalisation only (no ReLU on the last layer).
+__global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict__ img, int Hin, int Win,
+                                                         const float *__restrict__ w1blob, float *__restrict__ out)
+{
+    const int Ho = Hin - 2, Wo = Win - 2;
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (int64_t)Ho * Wo) return;
+    const int y = (int)(p / Wo), x = (int)(p % Wo);
+    const float *b1 = w1blob, *w1 = w1blob + NF;
+    float im[9];
+    for (int t = 0; t < 9; t++) im[t] = img[(size_t)(y + t / 3) * Win + x + t % 3];
+    float v[NF];
+    float ss = 0.0f;
+    for (int n = 0; n < NF; n++) {
+        float s = 0.0f;
+        for (int t = 0; t < 9; t++) s = fmaf(im[t], w1[t * NF + n], s);
+        v[n] = s + b1[n];
+        ss += v[n] * v[n];
+    }
+    const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+    for (int n = 0; n < NF; n++) out[p * NF + n] = v[n] * inv;
+}
+
+// Per-image statistics in double (mean, population std), one workgroup.
+__global__ __launch_bounds__(1024) void image_stats_kernel(const uint8_t *__restrict__ img, int64_t n,
+                                                           float *__restrict__ stats)
+{
+    __shared__ double red[1024];
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) s += img[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    const double mean = red[0] / (double)n;
+    __syncthreads();
+    double q = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) {
+        const double dv = img[i] - mean;
+        q += dv * dv;
+    }
+    red[threadIdx.x] = q;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        stats[0] = (float)mean;
+        stats[1] = (float)sqrt(red[0] / (double)n);
+    }
+}
+
+__global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restrict__ img, int H, int W, int pad,
+                                                        const float *__restrict__ stats, float *__restrict__ out)
+{
+    const int Wp = W + 2 * pad;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)(H + 2 * pad) * Wp) return;
+    const int y = (int)(i / Wp) - pad, x = (int)(i % Wp) - pad;
+    float v = 0.0f;
+    if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - stats[0]) / stats[1];
+    out[i] = v;
+}
+
+}  // namespace sde
+
+using namespace sde;
+
+static constexpr size_t TW_SMEM = (size_t)(TW_NPIX * 32 + 2 * NF * 32) * sizeof(float2);
+
+SDE_EXPORT int64_t sde_tower_packed_floats(int nlayers, int nf)
+{
+    if (nlayers < 1 || nf != NF) return -1;
+    return (int64_t)L1_FLOATS + (int64_t)(nlayers - 1) * LK_FLOATS;
+}
+
+SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *const *biases, int nlayers, int nf,
+                                      float *packed)
+{
+    if (!hwio || !biases || !packed || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
+    float *o = packed;
+    // layer 1: HWIO [3][3][1][64] is already [tap][n]
+    for (int n = 0; n < NF; n++) o[n] = biases[0][n];
+    for (int i = 0; i < 9 * NF; i++) o[NF + i] = hwio[0][i];
+    o += L1_FLOATS;
+    for (int l = 1; l < nlayers; l++) {
+        for (int n = 0; n < NF; n++) o[n] = biases[l][n];
+        float *w = o + NF;
+        for (int tap = 0; tap < 9; tap++)
+            for (int c = 0; c < NF; c++)
+                for (int n = 0; n < NF; n++)
+                    w[((size_t)tap * NF + n) * NF + c] = hwio[l][((size_t)tap * NF + c) * NF + n];
+        o += LK_FLOATS;
+    }
+    return SDE_OK;
+}
+
+SDE_EXPORT int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf)
+{
+    if (H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return -1;
+    if (nlayers <= 2) return 0;
+    // two ping-pong activation buffers sized for layer 2's output
+    const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
+    return 2 * h2 * w2 * NF * (int64_t)sizeof(float);
+}
+
+static void set_tower_attrs()
+{
+    static bool done = false;
+    if (done) return;
+    hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    done = true;
+}
+
+// One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
+// layer > 2 -> one 64->64 conv on Hin x Win x 64 activations.  Output (Hin-4|Hin-2) x ... x 64.
+static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
+                         hipStream_t st)
+{
+    set_tower_attrs();
+    const bool last = (layer == nlayers);
+    const float *w1 = packed;
+    const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
+    if (layer == 2) {
+        const int hout = Hin - 4, wout = Win - 4;
+        dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
+        if (last) conv64_mfma_kernel<true, true><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, w1, wk, out, hout, wout);
+        else conv64_mfma_kernel<true, false><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, w1, wk, out, hout, wout);
+    } else {
+        const int hout = Hin - 2, wout = Win - 2;
+        dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
+        if (last) conv64_mfma_kernel<false, true><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, nullptr, wk, out, hout, wout);
+        else conv64_mfma_kernel<false, false><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, nullptr, wk, out, hout, wout);
+    }
+}
+
+SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
+                               float *out, void *stream)
+{
+    if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
+    if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, as_stream(stream));
+    return launch_status();
+}
+
+SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
+                                 float *feat, void *workspace, int64_t workspace_bytes, void *stream)
+{
+    if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
+    const int64_t need = sde_tower_workspace_bytes(H, W, nlayers, nf);
+    if (need > 0 && (!workspace || workspace_bytes < need)) return SDE_ERR_WORKSPACE;
+    hipStream_t st = as_stream(stream);
+    const int Hp = H + 2 * nlayers, Wp = W + 2 * nlayers;
+    if (nlayers == 1) {
+        conv1_only_kernel<<<cdiv((int64_t)H * W, 256), 256, 0, st>>>(img_pad, Hp, Wp, packed, feat);
+        return launch_status();
+    }
+    float *buf[2] = {nullptr, nullptr};
+    if (nlayers > 2) {
+        const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
+        buf[0] = reinterpret_cast<float *>(workspace);
+        buf[1] = buf[0] + h2 * w2 * NF;
+    }
+    int hin = Hp, win = Wp;
+    launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], st);
+    hin -= 4; win -= 4;
+    int cur = 0;
+    for (int l = 3; l <= nlayers; l++) {
+        float *o = (l == nlayers) ? feat : buf[cur ^ 1];
+        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, st);
+        hin -= 2; win -= 2;
+        cur ^= 1;
+    }
+    return launch_status();
+}
+
+SDE_EXPORT int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, float *stats,
+                                 void *stream)
+{
+    if (!img || !out_pad || !stats || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
+    hipStream_t st = as_stream(stream);
+    image_stats_kernel<<<1, 1024, 0, st>>>(img, (int64_t)H * W, stats);
+    const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
+    znorm_pad_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, H, W, pad, stats, out_pad);
+    return launch_status();
+}

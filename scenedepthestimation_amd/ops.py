@@ -1,0 +1,261 @@
+"""Tensor-level wrappers over the C ABI (include/sde.h).
+
+Every op takes CUDA (HIP) torch tensors, checks dtype / contiguity / shape on
+the host, launches on torch's current stream and returns torch tensors.  torch
+is only plumbing here (device memory, streams); all arithmetic runs in the HIP
+kernels of libsde.so.  There is no CPU fallback: on a machine without a GPU
+these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import (SDE_LAYOUT_DHW, SDE_LAYOUT_HWD, SDE_SIDE_LEFT, SDE_SIDE_RIGHT, SDE_WTA_INIT_D0,
+                   SDE_WTA_INIT_INF, check, lib)
+
+LAYOUTS = {"DHW": SDE_LAYOUT_DHW, "HWD": SDE_LAYOUT_HWD}
+RULES = {"inf": SDE_WTA_INIT_INF, "d0": SDE_WTA_INIT_D0}
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need(t: torch.Tensor, name: str, dtype=torch.float32, shape=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must live on the GPU (got {t.device}); libsde has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)} (got {tuple(t.shape)})")
+    return t.data_ptr()
+
+
+def _empty(shape, dtype, like):
+    return torch.empty(shape, dtype=dtype, device=like.device)
+
+
+def _feat_pair(fl, fr):
+    if fl.dim() != 3 or tuple(fl.shape) != tuple(fr.shape):
+        raise ValueError(f"features must be matching [H,W,C] tensors, got {tuple(fl.shape)} / {tuple(fr.shape)}")
+    H, W, C = fl.shape
+    return _need(fl, "featuresl", shape=(H, W, C)), _need(fr, "featuresr", shape=(H, W, C)), H, W, C
+
+
+# ----------------------------------------------------------------------------
+# cost volume / WTA (process_functional.py:48-131, 800-837)
+# ----------------------------------------------------------------------------
+def cost_volume(fl, fr, ndisp: int, layout: str = "DHW", right: bool = False, invalid=None,
+                out_left=None, out_right=None):
+    """Exact cost volume.  DHW: compute_cost_volume (invalid -0.0).  HWD: GPU-path layout
+    with left and optionally right volumes (invalid 1.0, process_functional.py:1111)."""
+    pl, pr, H, W, C = _feat_pair(fl, fr)
+    lay = LAYOUTS[layout]
+    if invalid is None:
+        invalid = -0.0 if layout == "DHW" else 1.0
+    shape = (ndisp, H, W) if layout == "DHW" else (H, W, ndisp)
+    if out_left is None:
+        out_left = _empty(shape, torch.float32, fl)
+    ol = _need(out_left, "out_left", shape=shape)
+    orr = None
+    sides = SDE_SIDE_LEFT
+    if right:
+        if layout != "HWD":
+            raise ValueError("the right volume exists in the HWD (GPU-path) layout only")
+        if out_right is None:
+            out_right = _empty(shape, torch.float32, fl)
+        orr = _need(out_right, "out_right", shape=shape)
+        sides |= SDE_SIDE_RIGHT
+    check(lib.sde_cost_volume(pl, pr, H, W, C, int(ndisp), lay, sides, ctypes.c_float(invalid), ol, orr,
+                              _stream()), "sde_cost_volume")
+    return (out_left, out_right) if right else out_left
+
+
+def cv_wta(fl, fr, d0: int, d1: int, disp=None, min_cost=None, argmin=None, want=("disp",)):
+    """Fused cost volume + first-min over [d0, d1): WTA1(compute_cost_volume(fl, fr, d1)) when d0 = 0."""
+    pl, pr, H, W, C = _feat_pair(fl, fr)
+    if "disp" in want and disp is None:
+        disp = _empty((H, W), torch.float32, fl)
+    if "min" in want and min_cost is None:
+        min_cost = _empty((H, W), torch.float32, fl)
+    if "argmin" in want and argmin is None:
+        argmin = _empty((H, W), torch.int32, fl)
+    pd = _need(disp, "disp", shape=(H, W)) if disp is not None else None
+    pm = _need(min_cost, "min_cost", shape=(H, W)) if min_cost is not None else None
+    pa = _need(argmin, "argmin", dtype=torch.int32, shape=(H, W)) if argmin is not None else None
+    check(lib.sde_cv_wta(pl, pr, H, W, C, int(d0), int(d1), pd, pm, pa, _stream()), "sde_cv_wta")
+    return disp, min_cost, argmin
+
+
+def wta(vol, layout: str = "DHW", rule: str = "inf", out=None):
+    """First-min over d: WTA1 (DHW), WTA (HWD) or the SGM WTA kernel (HWD, rule='d0')."""
+    if vol.dim() != 3:
+        raise ValueError("volume must be 3-D")
+    if layout == "DHW":
+        D, H, W = vol.shape
+    else:
+        H, W, D = vol.shape
+    pv = _need(vol, "volume")
+    if out is None:
+        out = _empty((H, W), torch.float32, vol)
+    po = _need(out, "disp", shape=(H, W))
+    check(lib.sde_wta(pv, H, W, D, LAYOUTS[layout], RULES[rule], po, _stream()), "sde_wta")
+    return out
+
+
+def argmin_merge(mins, args, out=None):
+    """Ordered merge of per-shard (min [S,H,W], argmin [S,H,W]) -> float32 disparity [H,W]."""
+    S = mins.shape[0]
+    pm = _need(mins, "mins")
+    pa = _need(args, "args", dtype=torch.int32, shape=tuple(mins.shape))
+    npix = int(np.prod(mins.shape[1:]))
+    if out is None:
+        out = _empty(tuple(mins.shape[1:]), torch.float32, mins)
+    po = _need(out, "disp")
+    check(lib.sde_argmin_merge(pm, pa, S, npix, po, _stream()), "sde_argmin_merge")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# MC-CNN tower (mc_cnn_brunch.py:31-48) and preprocessing (match_single.py:34-43)
+# ----------------------------------------------------------------------------
+def tower_packed_floats(nlayers: int, nf: int = 64) -> int:
+    n = lib.sde_tower_packed_floats(nlayers, nf)
+    if n < 0:
+        raise ValueError(f"unsupported tower shape nlayers={nlayers} nf={nf}")
+    return int(n)
+
+
+def pack_tower_weights(hwio_list, bias_list) -> np.ndarray:
+    """Pack HWIO weights / biases (host numpy) into the device blob layout (host-side C helper)."""
+    L = len(hwio_list)
+    nf = int(hwio_list[0].shape[-1])
+    ws = [np.ascontiguousarray(w, dtype=np.float32) for w in hwio_list]
+    bs = [np.ascontiguousarray(b, dtype=np.float32) for b in bias_list]
+    for l, (w, b) in enumerate(zip(ws, bs)):
+        cin = 1 if l == 0 else nf
+        if w.shape != (3, 3, cin, nf) or b.shape != (nf,):
+            raise ValueError(f"layer {l + 1}: expected weights (3,3,{cin},{nf}) and biases ({nf},), "
+                             f"got {w.shape} / {b.shape}")
+    out = np.empty(tower_packed_floats(L, nf), np.float32)
+    wp = (ctypes.c_void_p * L)(*[w.ctypes.data for w in ws])
+    bp = (ctypes.c_void_p * L)(*[b.ctypes.data for b in bs])
+    check(lib.sde_tower_pack_weights(wp, bp, L, nf, out.ctypes.data), "sde_tower_pack_weights")
+    return out
+
+
+def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
+    return int(lib.sde_tower_workspace_bytes(H, W, nlayers, nf))
+
+
+def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None):
+    """img_pad: f32 [H+2L, W+2L] -> L2-normalised features f32 [H, W, nf]."""
+    Hp, Wp = img_pad.shape
+    H, W = Hp - 2 * nlayers, Wp - 2 * nlayers
+    if H <= 0 or W <= 0:
+        raise ValueError("padded image smaller than the tower's receptive field")
+    pi = _need(img_pad, "img_pad")
+    pw = _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),))
+    if out is None:
+        out = _empty((H, W, nf), torch.float32, img_pad)
+    po = _need(out, "features", shape=(H, W, nf))
+    need = tower_workspace_bytes(H, W, nlayers, nf)
+    if need > 0 and workspace is None:
+        workspace = torch.empty(need, dtype=torch.uint8, device=img_pad.device)
+    pws = _need(workspace, "workspace", dtype=torch.uint8) if need > 0 else None
+    wsb = workspace.numel() if need > 0 else 0
+    check(lib.sde_tower_forward(pi, H, W, pw, nlayers, nf, po, pws, wsb, _stream()), "sde_tower_forward")
+    return out
+
+
+def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64):
+    """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image)."""
+    if layer == 2:
+        Hin, Win = inp.shape
+        oshape = (Hin - 4, Win - 4, nf)
+    else:
+        Hin, Win, _ = inp.shape
+        oshape = (Hin - 2, Win - 2, nf)
+    check(lib.sde_tower_layer(_need(inp, "layer input"), Hin, Win,
+                              _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
+                              nlayers, nf, layer, _need(out, "layer output", shape=oshape), _stream()),
+          "sde_tower_layer")
+    return out
+
+
+def preprocess_u8(img_u8, pad: int, out=None, stats=None):
+    """u8 [H,W] -> zero-padded z-normalised f32 [H+2p, W+2p] on the device."""
+    H, W = img_u8.shape
+    pi = _need(img_u8, "image", dtype=torch.uint8)
+    if out is None:
+        out = _empty((H + 2 * pad, W + 2 * pad), torch.float32, img_u8)
+    if stats is None:
+        stats = _empty((2,), torch.float32, img_u8)
+    check(lib.sde_preprocess_u8(pi, H, W, pad, _need(out, "out_pad", shape=(H + 2 * pad, W + 2 * pad)),
+                                _need(stats, "stats", shape=(2,)), _stream()), "sde_preprocess_u8")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# SGM and post-processing (process_functional.py:134-1088)
+# ----------------------------------------------------------------------------
+def sgm_penalties(img_u8, P1=2.3, P2=55.9, threshold=30, lamda=4, out=None):
+    H, W = img_u8.shape
+    pi = _need(img_u8, "image", dtype=torch.uint8)
+    if out is None:
+        out = _empty((H, W, 16), torch.float32, img_u8)
+    check(lib.sde_sgm_penalties(pi, H, W, float(P1), float(P2), int(threshold), float(lamda),
+                                _need(out, "penalties", shape=(H, W, 16)), _stream()), "sde_sgm_penalties")
+    return out
+
+
+def sgm_8path(cv_hwd, pen, S=None):
+    H, W, D = cv_hwd.shape
+    pc = _need(cv_hwd, "cost volume")
+    pp = _need(pen, "penalties", shape=(H, W, 16))
+    if S is None:
+        S = torch.zeros((H, W, D), dtype=torch.float32, device=cv_hwd.device)
+    check(lib.sde_sgm_8path(pc, pp, H, W, D, _need(S, "S", shape=(H, W, D)), _stream()), "sde_sgm_8path")
+    return S
+
+
+def sgm_direction(cv_hwd, pen, direction: int, S):
+    H, W, D = cv_hwd.shape
+    check(lib.sde_sgm_direction(_need(cv_hwd, "cost volume"), _need(pen, "penalties", shape=(H, W, 16)), H, W, D,
+                                int(direction), _need(S, "S", shape=(H, W, D)), _stream()), "sde_sgm_direction")
+    return S
+
+
+def lr_check(disp_l, disp_r, lrc_l=None, lrc_r=None):
+    H, W = disp_l.shape
+    if lrc_l is None:
+        lrc_l = torch.zeros((H, W), dtype=torch.uint8, device=disp_l.device)
+    if lrc_r is None:
+        lrc_r = torch.zeros((H, W), dtype=torch.uint8, device=disp_l.device)
+    check(lib.sde_lr_check(_need(disp_l, "disp_l"), _need(disp_r, "disp_r", shape=(H, W)), H, W,
+                           _need(lrc_l, "lrc_l", dtype=torch.uint8, shape=(H, W)),
+                           _need(lrc_r, "lrc_r", dtype=torch.uint8, shape=(H, W)), _stream()), "sde_lr_check")
+    return lrc_l, lrc_r
+
+
+def lrc_fill(disp_l, lrc_l, out=None):
+    H, W = disp_l.shape
+    if out is None:
+        out = _empty((H, W), torch.float32, disp_l)
+    check(lib.sde_lrc_fill(_need(disp_l, "disp_l"), _need(lrc_l, "lrc_l", dtype=torch.uint8, shape=(H, W)), H, W,
+                           _need(out, "out", shape=(H, W)), _stream()), "sde_lrc_fill")
+    return out
+
+
+def median5(src, dst):
+    H, W = src.shape
+    check(lib.sde_median5(_need(src, "src"), H, W, _need(dst, "dst", shape=(H, W)), _stream()), "sde_median5")
+    return dst

@@ -1,0 +1,116 @@
+"""Multi-GPU execution: one process per GPU, torch.distributed over RCCL (xGMI).
+
+The reference has no parallelism; two schemes are added:
+
+* pair data-parallel (config 4): rank r matches pairs r, r+N, ...; no
+  collective on the data path (``pairs_for_rank``).
+* disparity-sharded cost volume (config 5, north star): rank r owns the
+  disparity block ``shard_range(D, N, r)``.  Each rank computes the MC-CNN
+  features of a band of rows (+ the tower's halo) and one
+  ``all_gather_into_tensor`` assembles the full feature maps; each rank runs the
+  fused cost volume + first-min over its block, and a single all-gather of the
+  8-byte per-pixel partials (min f32, argmin i32) feeds an ordered merge
+  (strict `<` in rank order == lowest d on ties), so the result is bit-identical
+  to WTA1(compute_cost_volume(...)) on one device.
+
+The collectives are plain torch.distributed calls, so the same code runs on
+gloo (CPU tests) and nccl (= RCCL on ROCm).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(D: int, nshards: int, s: int):
+    """Contiguous, ordered disparity block of shard s: [s*D//n, (s+1)*D//n)."""
+    if not 0 <= s < nshards:
+        raise ValueError("shard index out of range")
+    return (s * D) // nshards, ((s + 1) * D) // nshards
+
+
+def row_band(H: int, nshards: int, s: int):
+    """Equal-height row bands (the last may be short) -> (r0, r1, rows_per_band)."""
+    rpb = (H + nshards - 1) // nshards
+    r0 = min(H, s * rpb)
+    return r0, min(H, r0 + rpb), rpb
+
+
+def pairs_for_rank(npairs: int, world: int, rank: int):
+    return list(range(rank, npairs, world))
+
+
+def init_from_env(backend: str | None = None):
+    """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def gather_partials(min_local: torch.Tensor, arg_local: torch.Tensor, world: int, group=None):
+    """One all-gather of the per-pixel (min f32, argmin i32) partials -> ([N,H,W] f32, [N,H,W] i32)."""
+    shape = tuple(min_local.shape)
+    npix = min_local.numel()
+    packed = torch.empty((2, npix), dtype=torch.int32, device=min_local.device)
+    packed[0] = min_local.reshape(-1).view(torch.int32)
+    packed[1] = arg_local.reshape(-1)
+    out = torch.empty((world, 2, npix), dtype=torch.int32, device=min_local.device)
+    dist.all_gather_into_tensor(out, packed, group=group)
+    mins = out[:, 0].contiguous().view(torch.float32).reshape((world,) + shape)
+    args = out[:, 1].contiguous().reshape((world,) + shape)
+    return mins, args
+
+
+def gather_row_bands(band: torch.Tensor, full: torch.Tensor, world: int, group=None):
+    """All-gather equal-height row bands [rpb, ...] into full [world*rpb, ...]."""
+    dist.all_gather_into_tensor(full, band, group=group)
+    return full
+
+
+class DisparityShardedMatcher:
+    """Config 5: features from row bands + all-gather, disparity-sharded fused CV/WTA + all-gather merge."""
+
+    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None):
+        from .pipeline import StereoMatcher
+        self.H, self.W, self.D = H, W, D
+        self.rank, self.world, self.group = rank, world, group
+        self.d_range = shard_range(D, world, rank)
+        self.m = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, d_range=self.d_range)
+        self.r0, self.r1, self.rpb = row_band(H, world, rank)
+        dev = self.m.device
+        self.band = torch.zeros((2, self.rpb, W, nf), dtype=torch.float32, device=dev)
+        self.full = torch.empty((world, 2, self.rpb, W, nf), dtype=torch.float32, device=dev)
+        self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
+
+    def features(self):
+        from . import ops
+        m, L = self.m, self.m.nlayers
+        for i in range(2):
+            ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
+            if self.r1 > self.r0:
+                # padded rows [r0, r1 + 2L) produce feature rows [r0, r1)
+                sub = m.img_pad[i][self.r0:self.r1 + 2 * L]
+                ops.tower_forward(sub, m.packed, L, m.nf, out=self.band[i, :self.r1 - self.r0], workspace=m.ws)
+        dist.all_gather_into_tensor(self.full, self.band, group=self.group)
+        for i in range(2):
+            m.feat[i].copy_(self.full[:, i].reshape(self.world * self.rpb, self.W, m.nf)[:self.H])
+        return m.feat[0], m.feat[1]
+
+    def match(self):
+        from . import ops
+        self.features()
+        _, mn, am = self.m.cost_wta(want=("min", "argmin"))
+        mins, args = gather_partials(mn, am, self.world, self.group)
+        return ops.argmin_merge(mins, args, out=self.disp)

@@ -1,0 +1,145 @@
+"""Device-resident stereo matching: buffers allocated once, every stage a libsde launch.
+
+``StereoMatcher`` is the hot path behind both the drop-in function API
+(process_functional.py) and bench.py:
+
+    u8 images (HBM) -> z-norm + zero pad -> MC-CNN tower (x2) -> fused cost
+    volume + WTA over [d0, d1)                         (configs 1/2, north star)
+
+and the GPU path of ``disparity_compute_by_gpu`` (process_functional.py:1093-1267):
+
+    features -> [H,W,D] L/R volumes -> penalties -> 8-path SGM (L, R) -> WTA
+    -> LR check -> LRC fill -> 5x5 median
+
+All buffers are sized for one (H, W, D) problem and reused across calls, so a
+call allocates nothing and can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import mc_cnn, ops
+
+
+class StereoMatcher:
+    def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
+                 nf: int = 64, device=None, d_range=None, sgm: bool = False):
+        self.H, self.W, self.D = int(height), int(width), int(ndisp)
+        self.nlayers, self.nf = int(nlayers), int(nf)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.d0, self.d1 = (0, self.D) if d_range is None else (int(d_range[0]), int(d_range[1]))
+        w = mc_cnn.load_weights(weights, self.nlayers)
+        hw, hb = mc_cnn.layer_lists(w, self.nlayers)
+        packed = ops.pack_tower_weights(hw, hb)
+        dev = self.device
+        H, W, L = self.H, self.W, self.nlayers
+        self.packed = torch.from_numpy(packed).to(dev)
+        self.img_u8 = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.img_pad = [torch.empty((H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.stats = [torch.empty((2,), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.feat = [torch.empty((H, W, nf), dtype=torch.float32, device=dev) for _ in range(2)]
+        nws = ops.tower_workspace_bytes(H, W, L, nf)
+        self.ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
+        self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
+        self.min_cost = torch.empty((H, W), dtype=torch.float32, device=dev)
+        self.argmin = torch.empty((H, W), dtype=torch.int32, device=dev)
+        self.sgm_bufs = None
+        if sgm:
+            self._alloc_sgm()
+
+    # -- stages ----------------------------------------------------------------
+    def load_images(self, left_u8, right_u8):
+        """Host u8 [H,W] arrays (or device tensors) -> resident device images."""
+        for dst, src in zip(self.img_u8, (left_u8, right_u8)):
+            t = src if isinstance(src, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(src, np.uint8))
+            dst.copy_(t, non_blocking=False)
+
+    def features(self):
+        """Preprocess + tower for both images (compute_feature, process_functional.py:11-45)."""
+        for i in range(2):
+            ops.preprocess_u8(self.img_u8[i], self.nlayers, out=self.img_pad[i], stats=self.stats[i])
+            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws)
+        return self.feat[0], self.feat[1]
+
+    def features_from_padded(self):
+        """Tower only, on already-normalised padded images in self.img_pad."""
+        for i in range(2):
+            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws)
+        return self.feat[0], self.feat[1]
+
+    def cost_wta(self, want=("disp",)):
+        """Fused cost volume + WTA over this matcher's disparity range [d0, d1)."""
+        return ops.cv_wta(self.feat[0], self.feat[1], self.d0, self.d1,
+                          disp=self.disp if "disp" in want else None,
+                          min_cost=self.min_cost if "min" in want else None,
+                          argmin=self.argmin if "argmin" in want else None, want=())
+
+    def match(self):
+        """One pass of the hot path on the resident images: features + fused CV/WTA -> disparity."""
+        self.features()
+        self.cost_wta()
+        return self.disp
+
+    # -- GPU path of disparity_compute_by_gpu ---------------------------------
+    def _alloc_sgm(self):
+        H, W, D, dev = self.H, self.W, self.D, self.device
+        self.sgm_bufs = dict(
+            cv=[torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(2)],
+            pen=[torch.empty((H, W, 16), dtype=torch.float32, device=dev) for _ in range(2)],
+            S=[torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(2)],
+            disp=[torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(2)],
+            lrc=[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)],
+            disp_a=torch.empty((H, W), dtype=torch.float32, device=dev),
+        )
+
+    def sgm_path(self, fl=None, fr=None, img_l=None, img_r=None, timings=None, post=True):
+        """process_functional.py:1093-1267 on device tensors; returns (disp_l, disp_r).
+
+        timings: optional dict receiving per-stage seconds (synchronised)."""
+        import time
+        if self.sgm_bufs is None:
+            self._alloc_sgm()
+        b = self.sgm_bufs
+        fl = self.feat[0] if fl is None else fl
+        fr = self.feat[1] if fr is None else fr
+        img_l = self.img_u8[0] if img_l is None else img_l
+        img_r = self.img_u8[1] if img_r is None else img_r
+
+        def mark(name, t0):
+            if timings is not None:
+                torch.cuda.synchronize(self.device)
+                t1 = time.time()
+                timings[name] = timings.get(name, 0.0) + (t1 - t0)
+                return t1
+            return t0
+
+        t = time.time() if timings is not None else 0.0
+        ops.cost_volume(fl, fr, self.D, layout="HWD", right=True, invalid=1.0,
+                        out_left=b["cv"][0], out_right=b["cv"][1])
+        t = mark("cost_volume", t)
+        ops.sgm_penalties(img_l, out=b["pen"][0])
+        ops.sgm_penalties(img_r, out=b["pen"][1])
+        for k in range(2):
+            b["S"][k].zero_()
+            ops.sgm_8path(b["cv"][k], b["pen"][k], S=b["S"][k])
+        t = mark("sgm", t)
+        for k in range(2):
+            ops.wta(b["S"][k], layout="HWD", rule="d0", out=b["disp"][k])
+        t = mark("wta", t)
+        if not post:
+            return b["disp"][0], b["disp"][1]
+        b["lrc"][0].zero_()
+        b["lrc"][1].zero_()
+        ops.lr_check(b["disp"][0], b["disp"][1], b["lrc"][0], b["lrc"][1])
+        ops.lrc_fill(b["disp"][0], b["lrc"][0], out=b["disp_a"])
+        t = mark("lrc", t)
+        # Median_Filter_kernel(d_disparityl_a, d_disparityr_a, d_disparityl, d_disparityr) (:1250):
+        # the interior of disp_l becomes the median of the LRC-filled map.  The reference's
+        # right input d_disparityr_a is never written (:1227); here the right map is filtered
+        # from its own WTA output (documented divergence, parity unpinned).
+        disp_r_src = b["disp"][1].clone()
+        ops.median5(b["disp_a"], b["disp"][0])
+        ops.median5(disp_r_src, b["disp"][1])
+        mark("filter", t)
+        return b["disp"][0], b["disp"][1]
