@@ -135,9 +135,11 @@ int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int 
  * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):
  * u8 image -> (I - mean) / std (population std, float32) written into the
  * interior of the zero-padded buffer out_pad [(H+2*pad)][(W+2*pad)].
- * stats: 2 floats of device scratch (mean, std) written by the call.
+ * scratch: SDE_PREPROCESS_SCRATCH_BYTES of device memory (exact integer pixel
+ * sums; zeroed by the call on the stream).
  */
-int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, float *stats,
+#define SDE_PREPROCESS_SCRATCH_BYTES 16
+int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,
                       void *stream);
 
 /* ---------------------------------------------------------------------- */

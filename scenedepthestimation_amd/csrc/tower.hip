@@ -22,6 +22,8 @@
 // lane pair l, l^32) before the store.
 #include "sde_common.h"
 
+#include <algorithm>
+
 namespace sde {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -213,47 +215,62 @@ __global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict
     for (int n = 0; n < NF; n++) out[p * NF + n] = v[n] * inv;
 }
 
-// Per-image statistics in double (mean, population std), one workgroup.
-__global__ __launch_bounds__(1024) void image_stats_kernel(const uint8_t *__restrict__ img, int64_t n,
-                                                           float *__restrict__ stats)
+// Per-image statistics: exact integer sum and sum of squares of the u8 pixels
+// (one 64-bit atomic pair per workgroup), finalised in double by every reader.
+__global__ __launch_bounds__(256) void image_sums_kernel(const uint8_t *__restrict__ img, int64_t n,
+                                                         unsigned long long *__restrict__ sums)
 {
-    __shared__ double red[1024];
-    double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) s += img[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
+    unsigned long long s = 0, q = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 3 < n && ((reinterpret_cast<uintptr_t>(img + i) & 3) == 0)) {
+            const uint32_t w = *reinterpret_cast<const uint32_t *>(img + i);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const unsigned v = (w >> (8 * k)) & 255u;
+                s += v;
+                q += v * v;
+            }
+        } else {
+            for (int64_t k = i; k < n && k < i + 4; k++) {
+                const unsigned v = img[k];
+                s += v;
+                q += v * v;
+            }
+        }
     }
-    const double mean = red[0] / (double)n;
-    __syncthreads();
-    double q = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) {
-        const double dv = img[i] - mean;
-        q += dv * dv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        q += __shfl_xor(q, o, 64);
     }
-    red[threadIdx.x] = q;
+    __shared__ unsigned long long red[2][4];
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][wave] = s; red[1][wave] = q; }
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        stats[0] = (float)mean;
-        stats[1] = (float)sqrt(red[0] / (double)n);
+        unsigned long long ts = 0, tq = 0;
+        for (int w = 0; w < 4; w++) { ts += red[0][w]; tq += red[1][w]; }
+        atomicAdd(&sums[0], ts);
+        atomicAdd(&sums[1], tq);
     }
 }
 
+// (I - mean) / std in float32 (match_single.py:40-41), zero border (process_functional.py:13-19).
 __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restrict__ img, int H, int W, int pad,
-                                                        const float *__restrict__ stats, float *__restrict__ out)
+                                                        const unsigned long long *__restrict__ sums,
+                                                        float *__restrict__ out)
 {
     const int Wp = W + 2 * pad;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)(H + 2 * pad) * Wp) return;
+    const double n = (double)H * W;
+    const double mean_d = (double)sums[0] / n;
+    const double var_d = fmax((double)sums[1] / n - mean_d * mean_d, 0.0);
+    const float mean = (float)mean_d, stdv = (float)sqrt(var_d);
     const int y = (int)(i / Wp) - pad, x = (int)(i % Wp) - pad;
     float v = 0.0f;
-    if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - stats[0]) / stats[1];
+    if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - mean) / stdv;
     out[i] = v;
 }
 
@@ -372,13 +389,17 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
     return launch_status();
 }
 
-SDE_EXPORT int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, float *stats,
+SDE_EXPORT int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,
                                  void *stream)
 {
-    if (!img || !out_pad || !stats || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
+    if (!img || !out_pad || !scratch || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
     hipStream_t st = as_stream(stream);
-    image_stats_kernel<<<1, 1024, 0, st>>>(img, (int64_t)H * W, stats);
+    unsigned long long *sums = reinterpret_cast<unsigned long long *>(scratch);
+    if (hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return SDE_ERR_LAUNCH;
+    const int64_t npix = (int64_t)H * W;
+    const int blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(npix, 256 * 4 * 8)));
+    image_sums_kernel<<<blocks, 256, 0, st>>>(img, npix, sums);
     const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
-    znorm_pad_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, H, W, pad, stats, out_pad);
+    znorm_pad_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, H, W, pad, sums, out_pad);
     return launch_status();
 }

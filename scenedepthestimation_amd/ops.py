@@ -191,16 +191,21 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64):
     return out
 
 
+PREPROCESS_SCRATCH_BYTES = 16
+
+
 def preprocess_u8(img_u8, pad: int, out=None, stats=None):
-    """u8 [H,W] -> zero-padded z-normalised f32 [H+2p, W+2p] on the device."""
+    """u8 [H,W] -> zero-padded z-normalised f32 [H+2p, W+2p] on the device.
+    stats: optional uint8 scratch tensor of PREPROCESS_SCRATCH_BYTES bytes."""
     H, W = img_u8.shape
     pi = _need(img_u8, "image", dtype=torch.uint8)
     if out is None:
         out = _empty((H + 2 * pad, W + 2 * pad), torch.float32, img_u8)
     if stats is None:
-        stats = _empty((2,), torch.float32, img_u8)
+        stats = _empty((PREPROCESS_SCRATCH_BYTES,), torch.uint8, img_u8)
     check(lib.sde_preprocess_u8(pi, H, W, pad, _need(out, "out_pad", shape=(H + 2 * pad, W + 2 * pad)),
-                                _need(stats, "stats", shape=(2,)), _stream()), "sde_preprocess_u8")
+                                _need(stats, "scratch", dtype=torch.uint8, shape=(PREPROCESS_SCRATCH_BYTES,)),
+                                _stream()), "sde_preprocess_u8")
     return out
 
 

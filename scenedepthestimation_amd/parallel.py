@@ -66,8 +66,9 @@ def gather_partials(min_local: torch.Tensor, arg_local: torch.Tensor, world: int
     packed = torch.empty((2, npix), dtype=torch.int32, device=min_local.device)
     packed[0] = min_local.reshape(-1).view(torch.int32)
     packed[1] = arg_local.reshape(-1)
-    out = torch.empty((world, 2, npix), dtype=torch.int32, device=min_local.device)
+    out = torch.empty((world * 2, npix), dtype=torch.int32, device=min_local.device)   # concatenated form
     dist.all_gather_into_tensor(out, packed, group=group)
+    out = out.view(world, 2, npix)
     mins = out[:, 0].contiguous().view(torch.float32).reshape((world,) + shape)
     args = out[:, 1].contiguous().reshape((world,) + shape)
     return mins, args
@@ -91,7 +92,7 @@ class DisparityShardedMatcher:
         self.r0, self.r1, self.rpb = row_band(H, world, rank)
         dev = self.m.device
         self.band = torch.zeros((2, self.rpb, W, nf), dtype=torch.float32, device=dev)
-        self.full = torch.empty((world, 2, self.rpb, W, nf), dtype=torch.float32, device=dev)
+        self.full = torch.empty((world * 2, self.rpb, W, nf), dtype=torch.float32, device=dev)
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
 
     def features(self):
@@ -104,8 +105,9 @@ class DisparityShardedMatcher:
                 sub = m.img_pad[i][self.r0:self.r1 + 2 * L]
                 ops.tower_forward(sub, m.packed, L, m.nf, out=self.band[i, :self.r1 - self.r0], workspace=m.ws)
         dist.all_gather_into_tensor(self.full, self.band, group=self.group)
+        full = self.full.view(self.world, 2, self.rpb, self.W, m.nf)
         for i in range(2):
-            m.feat[i].copy_(self.full[:, i].reshape(self.world * self.rpb, self.W, m.nf)[:self.H])
+            m.feat[i].copy_(full[:, i].reshape(self.world * self.rpb, self.W, m.nf)[:self.H])
         return m.feat[0], m.feat[1]
 
     def match(self):

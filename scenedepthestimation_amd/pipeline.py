@@ -37,7 +37,7 @@ class StereoMatcher:
         self.packed = torch.from_numpy(packed).to(dev)
         self.img_u8 = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.img_pad = [torch.empty((H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.stats = [torch.empty((2,), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.stats = [torch.empty((ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.feat = [torch.empty((H, W, nf), dtype=torch.float32, device=dev) for _ in range(2)]
         nws = ops.tower_workspace_bytes(H, W, L, nf)
         self.ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)

@@ -1,0 +1,79 @@
+"""CPU: libsde.so loads, exports exactly what include/sde.h declares, and its host-side
+entry points behave (no GPU needed: argument checks return before any launch)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from scenedepthestimation_amd import _lib
+from scenedepthestimation_amd._build import LIB
+
+
+def test_header_and_binding_agree():
+    declared = set(_lib.header_functions())
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = set(_lib.header_functions()) - exported
+    assert not missing, missing
+    # nothing else leaks out of the C ABI (hidden visibility)
+    extra = {s for s in exported if s.startswith("sde_")} - set(_lib.header_functions())
+    assert not extra, extra
+
+
+def test_version_and_status_strings():
+    assert _lib.lib.sde_abi_version() == 1
+    assert _lib.lib.sde_status_string(0) == b"ok"
+    assert _lib.lib.sde_status_string(-1) == b"invalid argument"
+    assert _lib.lib.sde_status_string(-3) == b"workspace too small"
+
+
+def test_tower_packing_matches_layout():
+    from scenedepthestimation_amd import mc_cnn, ops
+    L = 3
+    w = mc_cnn.synthetic_weights(L, seed=5)
+    hw, hb = mc_cnn.layer_lists(w, L)
+    packed = ops.pack_tower_weights(hw, hb)
+    assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * (64 + 9 * 64 * 64)
+    assert np.array_equal(packed[:64], hb[0])
+    assert np.array_equal(packed[64:640], hw[0].reshape(-1))
+    for l in (1, 2):
+        base = 640 + (l - 1) * (64 + 9 * 4096)
+        assert np.array_equal(packed[base:base + 64], hb[l])
+        blob = packed[base + 64:base + 64 + 9 * 4096].reshape(9, 64, 64)      # [tap][n][c]
+        ref = hw[l].reshape(9, 64, 64).transpose(0, 2, 1)                     # HWIO [tap][c][n] -> [tap][n][c]
+        assert np.array_equal(blob, ref)
+    assert ops.tower_workspace_bytes(100, 80, 5) == 2 * 106 * 86 * 64 * 4
+    assert ops.tower_workspace_bytes(100, 80, 2) == 0
+
+
+def test_argument_validation_without_gpu():
+    lib = _lib.lib
+    ERR = -1
+    assert lib.sde_cost_volume(None, None, 4, 4, 64, 4, 0, 1, ctypes.c_float(0.0), None, None, None) == ERR
+    assert lib.sde_cost_volume(1, 1, 4, 4, 64, 4, 0, 2, ctypes.c_float(0.0), 1, 1, None) == ERR   # right needs HWD
+    assert lib.sde_cv_wta(1, 1, 4, 4, 64, 5, 5, 1, None, None, None) == ERR                        # empty shard
+    assert lib.sde_wta(1, 4, 4, 4, 7, 0, 1, None) == ERR                                            # bad layout
+    assert lib.sde_sgm_8path(1, 1, 1, 5, 8, 1, None) == ERR                                        # H < 2
+    assert lib.sde_sgm_8path(1, 1, 5, 5, 513, 1, None) == ERR                                      # D > 512
+    assert lib.sde_sgm_direction(1, 1, 5, 5, 8, 8, 1, None) == ERR                                 # direction
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, None, 0, None) == ERR                       # nf != 64
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, None, 0, None) == -3                        # workspace
+    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, None) == ERR                               # layer 1
+    assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
+    assert lib.sde_tower_packed_floats(0, 64) == -1
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    from scenedepthestimation_amd import ops
+    f = torch.zeros((2, 3, 64))
+    with pytest.raises(ValueError, match="GPU"):
+        ops.cv_wta(f, f, 0, 2)
+    with pytest.raises(ValueError, match="GPU"):
+        ops.cost_volume(f, f, 2)

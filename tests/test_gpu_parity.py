@@ -238,3 +238,42 @@ def test_disparity_compute_by_gpu_vs_oracle(gpu, oracle):
     filled = oracle.lrc_fill(wl, a)
     assert np.array_equal(dl, oracle.median5(filled, wl))
     assert np.array_equal(dr, oracle.median5(wr, wr))
+
+
+def test_dshard_matcher_rccl_world1(gpu, oracle):
+    """The disparity-sharded matcher's collectives on RCCL (one rank on the single-GPU box)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from scenedepthestimation_amd.parallel import DisparityShardedMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        H, W, D = 40, 80, 24
+        left, right, _ = stereo_pair(H, W, D, seed=5)
+        dm = DisparityShardedMatcher(H, W, D, 0, 1)
+        dm.m.load_images(left, right)
+        disp = host(dm.match())
+        fl, fr = host(dm.m.feat[0]), host(dm.m.feat[1])
+        assert np.array_equal(disp, oracle.WTA1(oracle.compute_cost_volume(fl, fr, D)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cli_match_single_end_to_end(gpu, tmp_path, monkeypatch):
+    from scenedepthestimation_amd import imageio, match_single
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    left, right, _ = stereo_pair(48, 96, 16, seed=9)
+    imageio.imwrite(str(tmp_path / "eval" / "left_3.png"), left)
+    imageio.imwrite(str(tmp_path / "eval" / "right_3.png"), right)
+    monkeypatch.chdir(tmp_path)
+    match_single.main(["-i", "3", "-g", "0", "--checkpoint", "synthetic", "--cpu-path", "--ndisp", "16"])
+    out = imageio.imread_gray(str(tmp_path / "result" / "11_11" / "ld3.png"))
+    assert out.shape == (48, 96) and out.max() < 16
+    match_single.main(["-i", "3", "-g", "0", "--checkpoint", "synthetic", "--ndisp", "16", "-f", "sgm"])
+    assert imageio.imread_gray(str(tmp_path / "result" / "sgm" / "ld3.png")).shape == (48, 96)

@@ -1,0 +1,56 @@
+"""Per-stage HIP-event timings of the GPU path (SGM etc.) at a given size; prints JSON lines."""
+import json
+import sys
+import os
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from scenedepthestimation_amd import ops  # noqa: E402
+from scenedepthestimation_amd.synthetic import features, stereo_pair  # noqa: E402
+
+
+def timeit(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return min(ts)
+
+
+def main(H=1024, W=1024, D=192):
+    fl = torch.from_numpy(features(H, W, seed=0)).cuda()
+    fr = torch.from_numpy(features(H, W, seed=1)).cuda()
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    il = torch.from_numpy(left).cuda()
+    vox = H * W * D
+    out = {"H": H, "W": W, "D": D}
+    cvl = torch.empty((H, W, D), device="cuda")
+    cvr = torch.empty((H, W, D), device="cuda")
+    cvd = torch.empty((D, H, W), device="cuda")
+    out["cv_dhw_ms"] = timeit(lambda: ops.cost_volume(fl, fr, D, "DHW", out_left=cvd))
+    out["cv_hwd_left_ms"] = timeit(lambda: ops.cost_volume(fl, fr, D, "HWD", out_left=cvl))
+    out["cv_hwd_lr_ms"] = timeit(lambda: ops.cost_volume(fl, fr, D, "HWD", right=True, out_left=cvl, out_right=cvr))
+    out["cv_wta_ms"] = timeit(lambda: ops.cv_wta(fl, fr, 0, D))
+    out["wta_dhw_ms"] = timeit(lambda: ops.wta(cvd, "DHW"))
+    out["wta_hwd_ms"] = timeit(lambda: ops.wta(cvl, "HWD", "d0"))
+    pen = ops.sgm_penalties(il)
+    out["penalties_ms"] = timeit(lambda: ops.sgm_penalties(il, out=pen))
+    S = torch.zeros((H, W, D), device="cuda")
+    for d in range(8):
+        out[f"sgm_dir{d}_ms"] = timeit(lambda: ops.sgm_direction(cvl, pen, d, S), reps=2)
+    out["sgm_8path_ms"] = timeit(lambda: ops.sgm_8path(cvl, pen, S=S), reps=2)
+    out["sgm_GBs_algorithmic"] = 96.0 * vox / (out["sgm_8path_ms"] * 1e-3) / 1e9
+    out["cv_dhw_GBs_algorithmic"] = 4.0 * H * W * (2 * 64 + D) / (out["cv_dhw_ms"] * 1e-3) / 1e9
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    args = [int(a) for a in sys.argv[1:4]]
+    main(*args)
