@@ -46,6 +46,7 @@ WORKLOADS = {
     "cv": (1024, 1024, 192, "cv_wta"),
 }
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+PEAK_BF16_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
 PEAK_VALU_F32_TOPS = 78.6     # non-fused f32 ops/s (one op per lane-slot; FMA counts 2 in the 157.3)
 NF = 64
@@ -93,7 +94,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     def tower(i, timed):
         e_t = t_tower.start() if timed else None
         ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
-        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i])
+        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i], precision=m.tower_precision)
         hin, win = H + 2 * L - 4, W + 2 * L - 4
         cur = 0
         for layer in range(3, L + 1):
@@ -103,7 +104,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
                 o = acts[cur ^ 1].view(-1)[: (hin - 2) * (win - 2) * NF].view(hin - 2, win - 2, NF)
             src = acts[cur].view(-1)[: hin * win * NF].view(hin, win, NF)
             e = t_conv.start() if (timed and layer == 3) else None
-            ops.tower_layer(src, m.packed, L, layer, o)
+            ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision)
             if e is not None:
                 t_conv.stop(e)
             hin, win = hin - 2, win - 2
@@ -164,6 +165,7 @@ def main():
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tower-precision", default="bf16x6", choices=["fp32", "bf16x6"])
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
@@ -175,7 +177,7 @@ def main():
 
     t_conv, t_cv, t_tower = Timer(), Timer(), Timer()
     if args.mode == "dshard" and world > 1:
-        dm = DisparityShardedMatcher(H, W, D, rank, world)
+        dm = DisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
         dm.m.load_images(left, right)
 
         def step(timed=False):
@@ -186,7 +188,7 @@ def main():
             return r
         pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
     else:
-        m = StereoMatcher(H, W, D)
+        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision)
         m.load_images(left, right)
         if what == "cv_wta":
             m.features()
@@ -231,13 +233,30 @@ def main():
             hout = H + 2 * (NLAYERS - 3)
             wout = W + 2 * (NLAYERS - 3)
             fl = conv_flops(hout, wout)
-            ach = fl / (conv_ms * 1e-3) / 1e12
             stages["tower_ms_per_image"] = t_tower.mean_ms()
             stages["conv_layer3_ms"] = conv_ms
-            roof = {"kernel": "conv64_mfma_kernel<false,false> (tower layer 3)", "bound": "mfma",
-                    "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
-                    "traffic": None,
-                    "per_launch": f"{fl / 1e9:.2f} GFLOP = 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
+            stages["conv_fp32_equiv_TFLOPs"] = fl / (conv_ms * 1e-3) / 1e12
+            if m.tower_precision == "bf16x6":
+                # six bf16 partial products per fp32 product: the roof is the dense bf16 MFMA rate
+                ach = 6 * fl / (conv_ms * 1e-3) / 1e12
+                roof = {"kernel": "conv64_x6_kernel<false,false> (tower layer 3, bf16x6)", "bound": "mfma",
+                        "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,
+                        "traffic": None,
+                        "per_launch": f"6 x {fl / 1e9:.2f} GFLOP bf16 (2*{hout}*{wout}*64*576 fp32-equivalent) "
+                                      f"over {conv_ms:.3f} ms"}
+            else:
+                ach = fl / (conv_ms * 1e-3) / 1e12
+                roof = {"kernel": "conv64_mfma_kernel<false,false> (tower layer 3, fp32)", "bound": "mfma",
+                        "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+                        "traffic": None,
+                        "per_launch": f"{fl / 1e9:.2f} GFLOP = 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
+            if m.tower_precision == "bf16x6":
+                # the same features through the fp32-MFMA tower: max |difference| on this very image
+                ref = torch.empty_like(m.feat[0])
+                ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=ref, workspace=m.ws, precision="fp32")
+                ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=m.feat[0], workspace=m.ws,
+                                  precision="bf16x6")
+                stages["tower_bf16x6_vs_fp32_max_abs"] = float((ref - m.feat[0]).abs().max().item())
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             roof = {"kernel": "cv64_kernel<LEFT,WTA> (fused exact cost volume + WTA)", "bound": "hbm",
@@ -259,6 +278,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_step, "ms_per_pair": ms_step / pairs_per_step * world
             if scaling == "weak" else ms_step,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "tower_arith": ("bf16x6: fp32 operands split exactly into 3 bf16 parts, 6 leading partial products on "
+                            "bf16 MFMA, fp32 accumulation (fp32-level error)") if args.tower_precision == "bf16x6"
+                           else "fp32 MFMA",
             "data": "synthetic (seeded textured pair, band disparity field; synthetic He-normal tower weights)",
             "config": {"workload": args.workload, "H": H, "W": W, "D": D, "C": NF, "nlayers": NLAYERS,
                        "pipeline": what, "global_batch": pairs_per_step, "parallelism": par},

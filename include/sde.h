@@ -100,7 +100,12 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
 /* process_functional.py:11-45).  nlayers 3x3 VALID convs, nf = 64 maps.     */
 /* ---------------------------------------------------------------------- */
 
-/* Number of floats of the packed (device-layout) weight blob. */
+/* Tower arithmetic (flags of sde_tower_forward / sde_tower_layer). */
+#define SDE_TOWER_FP32 0      /* v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation            */
+#define SDE_TOWER_BF16X6 1    /* fp32 operands split exactly into 3 bf16 parts, the 6 leading partial products
+                                 on v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level error, 2.67x rate */
+
+/* Number of floats of the packed (device-layout) weight blob (fp32 + pre-split bf16 planes). */
 int64_t sde_tower_packed_floats(int nlayers, int nf);
 
 /*
@@ -120,7 +125,7 @@ int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf);
  * pixel (mc_cnn_brunch.py:48).  packed: device copy of the packed weights.
  */
 int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
-                      float *feat, void *workspace, int64_t workspace_bytes, void *stream);
+                      float *feat, void *workspace, int64_t workspace_bytes, int flags, void *stream);
 
 /*
  * One layer of the tower as a single kernel launch (for per-layer timing and
@@ -129,7 +134,7 @@ int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, i
  * nf activations, out (Hin-2) x (Win-2) x nf.  Layer nlayers L2-normalises.
  */
 int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
-                    float *out, void *stream);
+                    float *out, int flags, void *stream);
 
 /*
  * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):

@@ -24,6 +24,7 @@ SDE_OK = 0
 SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
 SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
+SDE_TOWER_FP32, SDE_TOWER_BF16X6 = 0, 1
 
 # name -> (restype, argtypes); must cover every function declared in include/sde.h
 SIGNATURES = {
@@ -40,8 +41,8 @@ SIGNATURES = {
                                        c_void_p]),
     "sde_tower_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
     "sde_tower_forward": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                  c_int64, c_void_p]),
-    "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+                                  c_int64, c_int, c_void_p]),
+    "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
                                   c_void_p]),

@@ -23,6 +23,7 @@
 #include "sde_common.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace sde {
 
@@ -35,7 +36,9 @@ constexpr int TW_IX = TW_TX + 2;         // input tile cols
 constexpr int TW_NPIX = TW_IY * TW_IX;   // 340
 constexpr int NF = 64;                   // feature maps (the reference's num_of_conv_feature_maps)
 constexpr int L1_FLOATS = NF + 9 * NF;           // bias + [tap][n]
-constexpr int LK_FLOATS = NF + 9 * NF * NF;      // bias + [tap][n][c]
+constexpr int LK_W = 9 * NF * NF;                // one [tap][n][c] plane, elements
+// layer k >= 2: bias f32 [64] | W f32 [tap][n][c] | 3 bf16 planes [p][tap][n][c] (hi, mid, lo: W = hi+mid+lo)
+constexpr int LK_FLOATS = NF + LK_W + 3 * LK_W / 2;
 
 // float2 slot of channel pair `pair` (0..31) of pixel/row `p` in a swizzled 64-float row
 __device__ __forceinline__ int pslot(int p, int pair) { return p * 32 + (pair ^ (p & 31)); }
@@ -192,6 +195,197 @@ __global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restric
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x6: fp32-accurate conv on the bf16 MFMA (v_mfma_f32_32x32x16_bf16).
+// Every fp32 operand is split exactly into three bf16 parts, x = x0 + x1 + x2
+// (RNE; each residual is exact in f32), and the six partial products with
+// i + j <= 2 are accumulated in fp32 (the three dropped ones are < 2^-23 |ab|,
+// below one fp32 rounding of the product).  16x the fp32 MFMA rate / 6 terms =
+// 2.67x the fp32 matrix peak at fp32-level error.  Weights arrive pre-split
+// (host packing); activations are split in registers from the fp32 LDS tile.
+// Same tiling as conv64_mfma_kernel; LDS: fp32 tile (16-B XOR swizzle by pixel)
+// + double-buffered 3 x [64 n][64 c] bf16 weight planes (16-B swizzle by n>>1).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
+{
+    h = (__bf16)x;
+    const float r1 = x - (float)h;
+    m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    l = (__bf16)r2;
+}
+
+// tile image: pixel p, 16-B chunk q (channels 4q..4q+3)
+__device__ __forceinline__ int tslot(int p, int q) { return p * 16 + (q ^ (p & 15)); }
+// weight plane image: row n, 16-B chunk c8 (channels 8c8..8c8+7)
+__device__ __forceinline__ int wslot(int n, int c8) { return n * 8 + (c8 ^ ((n >> 1) & 7)); }
+
+constexpr int X6_TILE_BYTES = TW_NPIX * NF * 4;             // 87,040
+constexpr int X6_WBUF_BYTES = 3 * NF * NF * 2;              // 24,576 per tap buffer
+constexpr size_t X6_SMEM = (size_t)X6_TILE_BYTES + 2 * X6_WBUF_BYTES;
+
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(512) void conv64_x6_kernel(const float *__restrict__ in, int Hin, int Win,
+                                                        const float *__restrict__ w1blob,
+                                                        const float *__restrict__ wkblob,
+                                                        float *__restrict__ out, int Hout, int Wout)
+{
+    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
+    float4 *tile = smem4;                                                    // [340][16] float4
+    uint4 *wbuf0 = reinterpret_cast<uint4 *>(smem4 + X6_TILE_BYTES / 16);    // [3][64][8] uint4
+    uint4 *wbuf1 = wbuf0 + X6_WBUF_BYTES / 16;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int tx0 = blockIdx.x * TW_TX;
+    const int ty0 = blockIdx.y * TW_TY;
+    const float *bias = wkblob;
+    const uint4 *planes = reinterpret_cast<const uint4 *>(wkblob + NF + LK_W);   // [3][9][64][8] uint4
+
+    // weight prefetch: thread t moves chunk (n = t>>3, c8 = t&7) of each plane
+    const int wn = tid >> 3, wc8 = tid & 7;
+    const size_t wofs = (size_t)wn * 8 + wc8;
+    constexpr size_t PSTRIDE = (size_t)9 * NF * 8;      // uint4 per plane
+    uint4 wr0 = planes[wofs], wr1 = planes[PSTRIDE + wofs], wr2 = planes[2 * PSTRIDE + wofs];
+
+    if (!FIRST) {
+        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
+            const int p = idx >> 4, q = idx & 15;
+            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (iy < Hin && ix < Win) v = reinterpret_cast<const float4 *>(in + ((size_t)iy * Win + ix) * NF)[q];
+            tile[tslot(p, q)] = v;
+        }
+    } else {
+        const float *b1 = w1blob;
+        const float *w1 = w1blob + NF;
+        const int H1 = Hin - 2, W1 = Win - 2;
+        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
+            const int p = idx >> 4, q = idx & 15;
+            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (iy < H1 && ix < W1) {
+                float im[9];
+#pragma unroll
+                for (int t = 0; t < 9; t++) im[t] = in[(size_t)(iy + t / 3) * Win + ix + t % 3];
+                float a[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int n = 4 * q + j;
+                    float s = 0.0f;
+#pragma unroll
+                    for (int t = 0; t < 9; t++) s = fmaf(im[t], w1[t * NF + n], s);
+                    s += b1[n];
+                    a[j] = s > 0.0f ? s : 0.0f;
+                }
+                v = make_float4(a[0], a[1], a[2], a[3]);
+            }
+            tile[tslot(p, q)] = v;
+        }
+    }
+    {
+        const int ws = wslot(wn, wc8);
+        wbuf0[ws] = wr0;
+        wbuf0[NF * 8 + ws] = wr1;
+        wbuf0[2 * NF * 8 + ws] = wr2;
+    }
+    __syncthreads();
+
+    floatx16 acc0 = {0}, acc1 = {0};
+    const int j = lane & 31;
+    const int h = lane >> 5;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; tap++) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const uint4 *wb = (tap & 1) ? wbuf1 : wbuf0;
+        if (tap < 8) {
+            const size_t o = (size_t)(tap + 1) * NF * 8 + wofs;
+            wr0 = planes[o];
+            wr1 = planes[PSTRIDE + o];
+            wr2 = planes[2 * PSTRIDE + o];
+        }
+        const int p = (wave + ky) * TW_IX + (j + kx);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const float4 x0 = tile[tslot(p, 4 * s + 2 * h)];
+            const float4 x1 = tile[tslot(p, 4 * s + 2 * h + 1)];
+            const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            bf16x8 b0, b1, b2;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                __bf16 hh, mm, ll;
+                split3(xv[i], hh, mm, ll);
+                b0[i] = hh; b1[i] = mm; b2[i] = ll;
+            }
+            const int c8 = 2 * s + h;
+            const int s0 = wslot(j, c8), s1 = wslot(32 + j, c8);
+            const bf16x8 a00 = __builtin_bit_cast(bf16x8, wb[s0]);
+            const bf16x8 a01 = __builtin_bit_cast(bf16x8, wb[NF * 8 + s0]);
+            const bf16x8 a02 = __builtin_bit_cast(bf16x8, wb[2 * NF * 8 + s0]);
+            const bf16x8 a10 = __builtin_bit_cast(bf16x8, wb[s1]);
+            const bf16x8 a11 = __builtin_bit_cast(bf16x8, wb[NF * 8 + s1]);
+            const bf16x8 a12 = __builtin_bit_cast(bf16x8, wb[2 * NF * 8 + s1]);
+            // small terms first, the leading product last
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a02, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a12, b0, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a01, b1, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a11, b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b2, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b2, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a01, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a11, b0, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b1, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b0, acc1, 0, 0, 0);
+        }
+        if (tap < 8) {
+            uint4 *nb = (tap & 1) ? wbuf0 : wbuf1;
+            const int ws = wslot(wn, wc8);
+            nb[ws] = wr0;
+            nb[NF * 8 + ws] = wr1;
+            nb[2 * NF * 8 + ws] = wr2;
+        }
+        __syncthreads();
+    }
+
+    float v[2][16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int n = 8 * (r >> 2) + 4 * h + (r & 3);
+        v[0][r] = acc0[r] + bias[n];
+        v[1][r] = acc1[r] + bias[32 + n];
+    }
+    if (!LAST) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            v[0][r] = v[0][r] > 0.0f ? v[0][r] : 0.0f;
+            v[1][r] = v[1][r] > 0.0f ? v[1][r] : 0.0f;
+        }
+    } else {
+        float ss = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; r++) ss += v[0][r] * v[0][r] + v[1][r] * v[1][r];
+        ss += __shfl_xor(ss, 32, 64);
+        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+#pragma unroll
+        for (int r = 0; r < 16; r++) { v[0][r] *= inv; v[1][r] *= inv; }
+    }
+    const int oy = ty0 + wave, ox = tx0 + j;
+    if (oy < Hout && ox < Wout) {
+        float *dst = out + ((size_t)oy * Wout + ox) * NF;
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+                *reinterpret_cast<float4 *>(dst + mt * 32 + 8 * g + 4 * h) =
+                    make_float4(v[mt][4 * g], v[mt][4 * g + 1], v[mt][4 * g + 2], v[mt][4 * g + 3]);
+    }
+}
+
 // nlayers == 1: conv1 + L2 normalisation only (no ReLU on the last layer).
 __global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict__ img, int Hin, int Win,
                                                          const float *__restrict__ w1blob, float *__restrict__ out)
@@ -278,6 +472,23 @@ __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restric
 
 using namespace sde;
 
+static uint16_t f2bf_rne(float f)
+{
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);   // NaN stays NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+static float bf2f(uint16_t h)
+{
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
 static constexpr size_t TW_SMEM = (size_t)(TW_NPIX * 32 + 2 * NF * 32) * sizeof(float2);
 
 SDE_EXPORT int64_t sde_tower_packed_floats(int nlayers, int nf)
@@ -298,10 +509,21 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
     for (int l = 1; l < nlayers; l++) {
         for (int n = 0; n < NF; n++) o[n] = biases[l][n];
         float *w = o + NF;
+        uint16_t *pl = reinterpret_cast<uint16_t *>(w + LK_W);
         for (int tap = 0; tap < 9; tap++)
             for (int c = 0; c < NF; c++)
-                for (int n = 0; n < NF; n++)
-                    w[((size_t)tap * NF + n) * NF + c] = hwio[l][((size_t)tap * NF + c) * NF + n];
+                for (int n = 0; n < NF; n++) {
+                    const size_t dsti = ((size_t)tap * NF + n) * NF + c;
+                    const float x = hwio[l][((size_t)tap * NF + c) * NF + n];
+                    w[dsti] = x;
+                    const uint16_t h0 = f2bf_rne(x);
+                    const float r1 = x - bf2f(h0);
+                    const uint16_t h1 = f2bf_rne(r1);
+                    const float r2 = r1 - bf2f(h1);
+                    pl[dsti] = h0;
+                    pl[LK_W + dsti] = h1;
+                    pl[2 * (size_t)LK_W + dsti] = f2bf_rne(r2);
+                }
         o += LK_FLOATS;
     }
     return SDE_OK;
@@ -324,44 +546,51 @@ static void set_tower_attrs()
     hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    hipFuncSetAttribute((const void *)conv64_x6_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    hipFuncSetAttribute((const void *)conv64_x6_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    hipFuncSetAttribute((const void *)conv64_x6_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    hipFuncSetAttribute((const void *)conv64_x6_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
     done = true;
 }
 
 // One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
 // layer > 2 -> one 64->64 conv on Hin x Win x 64 activations.  Output (Hin-4|Hin-2) x ... x 64.
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
-                         hipStream_t st)
+                         int flags, hipStream_t st)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
+    const bool x6 = (flags & SDE_TOWER_BF16X6) != 0;
     const float *w1 = packed;
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
-    if (layer == 2) {
-        const int hout = Hin - 4, wout = Win - 4;
-        dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
-        if (last) conv64_mfma_kernel<true, true><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, w1, wk, out, hout, wout);
-        else conv64_mfma_kernel<true, false><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, w1, wk, out, hout, wout);
+    const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
+    dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
+#define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout)
+    if (x6) {
+        if (layer == 2) { if (last) SDE_CONV(conv64_x6_kernel, true, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, true, false, X6_SMEM); }
+        else { if (last) SDE_CONV(conv64_x6_kernel, false, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, false, false, X6_SMEM); }
     } else {
-        const int hout = Hin - 2, wout = Win - 2;
-        dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
-        if (last) conv64_mfma_kernel<false, true><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, nullptr, wk, out, hout, wout);
-        else conv64_mfma_kernel<false, false><<<grid, 512, TW_SMEM, st>>>(in, Hin, Win, nullptr, wk, out, hout, wout);
+        if (layer == 2) { if (last) SDE_CONV(conv64_mfma_kernel, true, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, true, false, TW_SMEM); }
+        else { if (last) SDE_CONV(conv64_mfma_kernel, false, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, false, false, TW_SMEM); }
     }
+#undef SDE_CONV
 }
 
 SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
-                               float *out, void *stream)
+                               float *out, int flags, void *stream)
 {
     if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
     if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
-    launch_layer(in, Hin, Win, packed, nlayers, layer, out, as_stream(stream));
+    if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, as_stream(stream));
     return launch_status();
 }
 
 SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
-                                 float *feat, void *workspace, int64_t workspace_bytes, void *stream)
+                                 float *feat, void *workspace, int64_t workspace_bytes, int flags, void *stream)
 {
     if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
+    if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
     const int64_t need = sde_tower_workspace_bytes(H, W, nlayers, nf);
     if (need > 0 && (!workspace || workspace_bytes < need)) return SDE_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
@@ -377,12 +606,12 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
         buf[1] = buf[0] + h2 * w2 * NF;
     }
     int hin = Hp, win = Wp;
-    launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], st);
+    launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, st);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
-        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, st);
+        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, st);
         hin -= 2; win -= 2;
         cur ^= 1;
     }

@@ -156,8 +156,12 @@ def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
     return int(lib.sde_tower_workspace_bytes(H, W, nlayers, nf))
 
 
-def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None):
-    """img_pad: f32 [H+2L, W+2L] -> L2-normalised features f32 [H, W, nf]."""
+TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6}
+
+
+def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None, precision: str = "fp32"):
+    """img_pad: f32 [H+2L, W+2L] -> L2-normalised features f32 [H, W, nf].
+    precision: 'fp32' (fp32 MFMA) or 'bf16x6' (exact 3-way bf16 split, 6 partial products, fp32 accumulate)."""
     Hp, Wp = img_pad.shape
     H, W = Hp - 2 * nlayers, Wp - 2 * nlayers
     if H <= 0 or W <= 0:
@@ -172,11 +176,12 @@ def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspa
         workspace = torch.empty(need, dtype=torch.uint8, device=img_pad.device)
     pws = _need(workspace, "workspace", dtype=torch.uint8) if need > 0 else None
     wsb = workspace.numel() if need > 0 else 0
-    check(lib.sde_tower_forward(pi, H, W, pw, nlayers, nf, po, pws, wsb, _stream()), "sde_tower_forward")
+    check(lib.sde_tower_forward(pi, H, W, pw, nlayers, nf, po, pws, wsb, TOWER_PRECISIONS[precision], _stream()),
+          "sde_tower_forward")
     return out
 
 
-def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64):
+def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32"):
     """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image)."""
     if layer == 2:
         Hin, Win = inp.shape
@@ -186,7 +191,8 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64):
         oshape = (Hin - 2, Win - 2, nf)
     check(lib.sde_tower_layer(_need(inp, "layer input"), Hin, Win,
                               _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
-                              nlayers, nf, layer, _need(out, "layer output", shape=oshape), _stream()),
+                              nlayers, nf, layer, _need(out, "layer output", shape=oshape),
+                              TOWER_PRECISIONS[precision], _stream()),
           "sde_tower_layer")
     return out
 

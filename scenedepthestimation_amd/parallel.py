@@ -83,12 +83,13 @@ def gather_row_bands(band: torch.Tensor, full: torch.Tensor, world: int, group=N
 class DisparityShardedMatcher:
     """Config 5: features from row bands + all-gather, disparity-sharded fused CV/WTA + all-gather merge."""
 
-    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None):
+    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="bf16x6"):
         from .pipeline import StereoMatcher
         self.H, self.W, self.D = H, W, D
         self.rank, self.world, self.group = rank, world, group
         self.d_range = shard_range(D, world, rank)
-        self.m = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, d_range=self.d_range)
+        self.m = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, d_range=self.d_range,
+                               tower_precision=tower_precision)
         self.r0, self.r1, self.rpb = row_band(H, world, rank)
         dev = self.m.device
         self.band = torch.zeros((2, self.rpb, W, nf), dtype=torch.float32, device=dev)
@@ -103,7 +104,8 @@ class DisparityShardedMatcher:
             if self.r1 > self.r0:
                 # padded rows [r0, r1 + 2L) produce feature rows [r0, r1)
                 sub = m.img_pad[i][self.r0:self.r1 + 2 * L]
-                ops.tower_forward(sub, m.packed, L, m.nf, out=self.band[i, :self.r1 - self.r0], workspace=m.ws)
+                ops.tower_forward(sub, m.packed, L, m.nf, out=self.band[i, :self.r1 - self.r0], workspace=m.ws,
+                                  precision=m.tower_precision)
         dist.all_gather_into_tensor(self.full, self.band, group=self.group)
         full = self.full.view(self.world, 2, self.rpb, self.W, m.nf)
         for i in range(2):

@@ -24,9 +24,12 @@ from . import mc_cnn, ops
 
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
-                 nf: int = 64, device=None, d_range=None, sgm: bool = False):
+                 nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6"):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)
         self.nlayers, self.nf = int(nlayers), int(nf)
+        if tower_precision not in ops.TOWER_PRECISIONS:
+            raise ValueError(f"tower_precision must be one of {sorted(ops.TOWER_PRECISIONS)}")
+        self.tower_precision = tower_precision
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.d0, self.d1 = (0, self.D) if d_range is None else (int(d_range[0]), int(d_range[1]))
         w = mc_cnn.load_weights(weights, self.nlayers)
@@ -59,13 +62,15 @@ class StereoMatcher:
         """Preprocess + tower for both images (compute_feature, process_functional.py:11-45)."""
         for i in range(2):
             ops.preprocess_u8(self.img_u8[i], self.nlayers, out=self.img_pad[i], stats=self.stats[i])
-            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws)
+            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
+                              precision=self.tower_precision)
         return self.feat[0], self.feat[1]
 
     def features_from_padded(self):
         """Tower only, on already-normalised padded images in self.img_pad."""
         for i in range(2):
-            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws)
+            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
+                              precision=self.tower_precision)
         return self.feat[0], self.feat[1]
 
     def cost_wta(self, want=("disp",)):

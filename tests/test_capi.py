@@ -39,15 +39,23 @@ def test_tower_packing_matches_layout():
     w = mc_cnn.synthetic_weights(L, seed=5)
     hw, hb = mc_cnn.layer_lists(w, L)
     packed = ops.pack_tower_weights(hw, hb)
-    assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * (64 + 9 * 64 * 64)
+    LW = 9 * 64 * 64
+    LK = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 planes
+    assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * LK
     assert np.array_equal(packed[:64], hb[0])
     assert np.array_equal(packed[64:640], hw[0].reshape(-1))
     for l in (1, 2):
-        base = 640 + (l - 1) * (64 + 9 * 4096)
+        base = 640 + (l - 1) * LK
         assert np.array_equal(packed[base:base + 64], hb[l])
-        blob = packed[base + 64:base + 64 + 9 * 4096].reshape(9, 64, 64)      # [tap][n][c]
+        blob = packed[base + 64:base + 64 + LW].reshape(9, 64, 64)            # [tap][n][c]
         ref = hw[l].reshape(9, 64, 64).transpose(0, 2, 1)                     # HWIO [tap][c][n] -> [tap][n][c]
         assert np.array_equal(blob, ref)
+        # the three bf16 planes sum exactly to the fp32 weight (RNE splits, exact residuals)
+        planes = packed[base + 64 + LW:base + LK].view(np.uint16).reshape(3, 9, 64, 64)
+        as_f32 = (planes.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        assert np.array_equal(as_f32.sum(0), ref.astype(np.float64))
+        hi = as_f32[0]
+        assert np.all(np.abs(ref - hi) <= np.abs(ref) * 2.0 ** -8)
     assert ops.tower_workspace_bytes(100, 80, 5) == 2 * 106 * 86 * 64 * 4
     assert ops.tower_workspace_bytes(100, 80, 2) == 0
 
@@ -62,9 +70,10 @@ def test_argument_validation_without_gpu():
     assert lib.sde_sgm_8path(1, 1, 1, 5, 8, 1, None) == ERR                                        # H < 2
     assert lib.sde_sgm_8path(1, 1, 5, 5, 513, 1, None) == ERR                                      # D > 512
     assert lib.sde_sgm_direction(1, 1, 5, 5, 8, 8, 1, None) == ERR                                 # direction
-    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, None, 0, None) == ERR                       # nf != 64
-    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, None, 0, None) == -3                        # workspace
-    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, None) == ERR                               # layer 1
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, None, 0, 0, None) == ERR                    # nf != 64
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, None, 0, 0, None) == -3                     # workspace
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 4, None) == ERR                 # bad flags
+    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, 0, None) == ERR                            # layer 1
     assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
     assert lib.sde_tower_packed_floats(0, 64) == -1
 

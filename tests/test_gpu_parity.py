@@ -131,8 +131,9 @@ def test_generic_channel_counts(gpu, golden, golden_cases):
 # ----------------------------------------------------------------------------
 # tower
 # ----------------------------------------------------------------------------
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 20, 37), (5, 41, 70), (3, 17, 33), (2, 9, 40), (1, 6, 7)])
-def test_tower_vs_oracle(gpu, oracle, nlayers, H, W):
+def test_tower_vs_oracle(gpu, oracle, nlayers, H, W, precision):
     from scenedepthestimation_amd import mc_cnn, ops
     rng = np.random.default_rng(nlayers * 1000 + H)
     w = mc_cnn.synthetic_weights(nlayers, seed=nlayers)
@@ -141,9 +142,28 @@ def test_tower_vs_oracle(gpu, oracle, nlayers, H, W):
     img[nlayers:-nlayers, nlayers:-nlayers] = rng.standard_normal((H, W)).astype(np.float32)
     ref = oracle.tower_forward(img, hw, hb)
     packed = dev(ops.pack_tower_weights(hw, hb))
-    out = host(ops.tower_forward(dev(img), packed, nlayers))
+    out = host(ops.tower_forward(dev(img), packed, nlayers, precision=precision))
     assert out.shape == ref.shape
     assert np.abs(out - ref).max() < 1e-4
+
+
+def test_tower_precision_report(gpu, oracle):
+    """Both tower arithmetics stay at fp32-level error vs the fp64 restatement (printed for the record)."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    rng = np.random.default_rng(77)
+    H, W, L = 64, 96, 5
+    w = mc_cnn.synthetic_weights(L)
+    hw, hb = mc_cnn.layer_lists(w, L)
+    img = np.zeros((H + 2 * L, W + 2 * L), np.float32)
+    img[L:-L, L:-L] = rng.standard_normal((H, W)).astype(np.float32)
+    ref = oracle.tower_forward(img, hw, hb)
+    packed = dev(ops.pack_tower_weights(hw, hb))
+    errs = {}
+    for prec in ("fp32", "bf16x6"):
+        out = host(ops.tower_forward(dev(img), packed, L, precision=prec))
+        errs[prec] = float(np.abs(out - ref).max())
+    print("tower max abs err vs fp64:", errs)
+    assert errs["fp32"] < 1e-5 and errs["bf16x6"] < 1e-5
 
 
 def test_preprocess_u8(gpu, oracle):
