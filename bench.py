@@ -166,6 +166,7 @@ def main():
     ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tower-precision", default="bf16x6", choices=["fp32", "bf16x6"])
+    ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
@@ -188,7 +189,7 @@ def main():
             return r
         pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
     else:
-        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision)
+        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
         m.load_images(left, right)
         if what == "cv_wta":
             m.features()
@@ -228,6 +229,9 @@ def main():
         stages["cv_wta_valu_Tops"] = 127.0 * vox / (cv_ms * 1e-3) / 1e12
         stages["cv_wta_valu_frac"] = stages["cv_wta_valu_Tops"] / PEAK_VALU_F32_TOPS
         stages["cv_wta_Mvox_s"] = vox / (cv_ms * 1e-3) / 1e6
+        stages["cv_mode"] = args.cv_mode
+        if args.cv_mode == "certified":
+            stages["cv_exact_fixup_pixels"] = ops.cv_wta_fixups(m.cv_ws)
         if what == "tower+cv_wta":
             conv_ms = t_conv.mean_ms()
             hout = H + 2 * (NLAYERS - 3)

@@ -77,15 +77,28 @@ int sde_cost_volume(const float *fl, const float *fr, int H, int W, int C, int D
  */
 int sde_wta(const float *vol, int H, int W, int D, int layout, int rule, float *disp, void *stream);
 
+/* sde_cv_wta modes: both give identical (bit-exact) outputs. */
+#define SDE_CV_EXACT 0       /* every voxel in NumPy's pairwise order on VALU                                */
+#define SDE_CV_CERTIFIED 1   /* bf16x3 MFMA scores + rigorous error bound; pixels whose winner is not
+                                certified by a 2*eps gap are resolved by the exact scan (needs workspace) */
+
+/* Workspace bytes sde_cv_wta needs in SDE_CV_CERTIFIED mode (work-list of unresolved pixels). */
+int64_t sde_cv_wta_workspace_bytes(int H, int W);
+
 /*
  * Fused cost volume + WTA over the disparity shard [d0, d1) without
  * materialising the volume: WTA1(compute_cost_volume(fl, fr, D)) bit-exact when
- * d0 = 0, d1 = D.  Outputs (each optional, NULL to skip): disp (float32 argmin),
- * min_cost (float32 first-min value) and argmin (int32, -1 if none), [H][W].
- * Shards merge bit-exactly with sde_argmin_merge (ties -> lower d).
+ * d0 = 0, d1 = D (process_functional.py:48-73 + :96-113).  Outputs (each
+ * optional, NULL to skip): disp (float32 argmin), min_cost (float32 first-min
+ * cost, bit-exact) and argmin (int32, -1 if none), [H][W].  Shards merge
+ * bit-exactly with sde_argmin_merge (ties -> lower d).  mode: SDE_CV_EXACT or
+ * SDE_CV_CERTIFIED (C == 64; other C always run exact).  The workspace's first
+ * 4 bytes hold, after the call, the number of pixels the certified mode
+ * resolved exactly.
  */
 int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, int d1, float *disp,
-               float *min_cost, int32_t *argmin, void *stream);
+               float *min_cost, int32_t *argmin, int mode, void *workspace, int64_t workspace_bytes,
+               void *stream);
 
 /*
  * Ordered merge of per-shard (min, argmin) pairs: shard s covers a disparity

@@ -25,6 +25,7 @@ SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
 SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
 SDE_TOWER_FP32, SDE_TOWER_BF16X6 = 0, 1
+SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
 
 # name -> (restype, argtypes); must cover every function declared in include/sde.h
 SIGNATURES = {
@@ -33,8 +34,9 @@ SIGNATURES = {
     "sde_cost_volume": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                 c_void_p, c_void_p, c_void_p]),
     "sde_wta": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_cv_wta_workspace_bytes": (c_int64, [c_int, c_int]),
     "sde_cv_wta": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                           c_void_p, c_void_p]),
+                           c_void_p, c_int, c_void_p, c_int64, c_void_p]),
     "sde_argmin_merge": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "sde_tower_packed_floats": (c_int64, [c_int, c_int]),
     "sde_tower_pack_weights": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int,

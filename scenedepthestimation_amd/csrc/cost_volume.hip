@@ -21,6 +21,8 @@
 // by (value, index) at the end, which equals the sequential scan.
 #include "sde_common.h"
 
+#include <algorithm>
+
 namespace sde {
 
 constexpr int CV_TX = 64;                    // own pixels per workgroup (= lanes)
@@ -249,6 +251,289 @@ __global__ __launch_bounds__(256) void argmin_merge_kernel(const float *__restri
     disp[p] = (float)arg;
 }
 
+// ===========================================================================
+// Certified fast path for the fused cost volume + WTA (north-star kernel).
+//
+// Scores s(x,d) = fl[x] . fr[x-d] are computed on the bf16 MFMA
+// (v_mfma_f32_32x32x16_bf16) with every fp32 operand split into hi + lo bf16
+// parts and the three leading partial products (hh, hl, lh) accumulated in
+// fp32.  Rigorous bound for every voxel of a pixel (Cauchy-Schwarz on |a|,|b|):
+//   |s_fast - s_true| <= (3*2^-16 + 192*2^-23) * sum|a_c b_c|   (split + accumulation)
+//   |s_exact - s_true| <= 10*2^-24 * sum|a_c b_c|               (NumPy pairwise order)
+//   => |s_fast - s_exact| <= FX_K * sum|a_c b_c| <= FX_K * ||fl[x]||_1 * max_window |fr|
+//      (FX_K = 1e-4: 1.4x margin over 7e-5)
+// If the best fast score beats the runner-up by more than 2 eps, the exact
+// first-min is provably the fast argmax (no other d can tie or win exactly),
+// and its exact cost is computed once (same arithmetic as cv64_kernel).  Any
+// other pixel (near-ties, NaN/Inf features) goes to a work list that
+// cv_wta_fixup_kernel resolves with the exact scan.  Outputs are therefore
+// bit-identical to the exact kernel for every input.
+//
+// Mapping: workgroup = 4 waves on one row and 64 left pixels (2 N-tiles of 32);
+// the right-feature window of a <=128-disparity chunk (<= 6 M-tiles of 32
+// pixels) is split once into hi/lo bf16 planes in LDS (16-B XOR swizzle by
+// pixel>>1); wave w owns N-tile w&1 and every other M-tile; the left operand
+// lives in registers (hi/lo, 32 VGPRs).  Blocks are remapped so all blocks of
+// a row run on one XCD (its L2 serves the overlapping windows).
+// ===========================================================================
+typedef __bf16 fx_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float fx_floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int FX_NX = 64;          // left pixels per workgroup
+constexpr int FX_DCH = 128;        // disparities per window chunk
+constexpr int FX_NT = 6;           // max M-tiles per chunk: ceil((128 + 63) / 32)
+constexpr int FX_WIN = FX_NT * 32; // window pixels
+constexpr float FX_K = 1e-4f;
+constexpr float FX_ABS = 1e-30f;   // absolute slack (bf16 subnormal handling)
+
+// Exact NumPy-order cost of two 64-float rows in global memory (16-B loads).
+__device__ __forceinline__ float dot64_exact_global(const float4 *__restrict__ a, const float4 *__restrict__ b)
+{
+    float acc[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        const float4 a0 = a[2 * m], a1 = a[2 * m + 1], b0 = b[2 * m], b1 = b[2 * m + 1];
+        const float p[8] = {a0.x * b0.x, a0.y * b0.y, a0.z * b0.z, a0.w * b0.w,
+                            a1.x * b1.x, a1.y * b1.y, a1.z * b1.z, a1.w * b1.w};
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) acc[jj] = (m == 0) ? p[jj] : acc[jj] + p[jj];
+    }
+    const float res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    return -(0.0f + res);
+}
+
+__device__ __forceinline__ int fx_slot(int r, int c8) { return r * 8 + (c8 ^ ((r >> 1) & 7)); }
+
+__device__ __forceinline__ void fx_split(float x, __bf16 &h, __bf16 &l)
+{
+    h = (__bf16)x;
+    l = (__bf16)(x - (float)h);
+}
+
+// merge (best, arg, second) of two disjoint candidate sets, scores in max-domain
+__device__ __forceinline__ void fx_merge(float &b, int &a, float &s, float b2, int a2, float s2)
+{
+    const float ns = fmaxf(fminf(b, b2), fmaxf(s, s2));
+    if (b2 > b || (b2 == b && a2 < a)) { b = b2; a = a2; }
+    s = ns;
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    // bijective: blocks b, b+8, ... (one XCD under round-robin dispatch) get consecutive logical ids
+    const int q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// One workgroup per (row, 64-pixel strip); 3 workgroups per CU (<= 168 VGPRs,
+// 50 KB LDS) hide each other's memory latency.  Every global load of a
+// workgroup is issued up front from clamped addresses (no per-element
+// branches), so a workgroup pays about one memory round trip.
+//
+// Error bound per pixel: sum_c |a_c b_c| <= ||a||_1 * max_window |b|, so
+// eps = FX_K * ||fl[x]||_1 * ||fr window||_inf + FX_ABS needs no cross-lane
+// norm reductions while staging.
+//
+// Top-2 tracking per lane in 4 independent states (register r -> state r&3)
+// for ILP: best' = max(best, v), second' = med3(best, second, v) (best >=
+// second), arg' = v > best ? d : arg.
+__global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                             int H, int W, int d0, int d1,
+                                                             float *__restrict__ out_min, int32_t *__restrict__ out_arg,
+                                                             float *__restrict__ out_disp, unsigned *__restrict__ counter,
+                                                             int32_t *__restrict__ list)
+{
+    __shared__ uint4 pl_hi[FX_WIN * 8];
+    __shared__ uint4 pl_lo[FX_WIN * 8];
+    __shared__ float mb[4][64];
+    __shared__ int ma[4][64];
+    __shared__ float ms[4][64];
+    __shared__ unsigned binf_bits;
+
+    const int nbx = (W + FX_NX - 1) / FX_NX;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int y = lb / nbx;
+    const int x0 = (lb % nbx) * FX_NX;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = wave & 1, mpar = wave >> 1;
+    const int j = lane & 31, h = lane >> 5;
+    const int x = x0 + 32 * n + j;
+    const bool xok = x < W;
+    const float4 *frow = reinterpret_cast<const float4 *>(fr + (size_t)y * W * 64);
+
+    if (tid == 0) binf_bits = 0u;
+
+    // ---- left operand (8 float4 per lane), split hi/lo; ||a||_1 ------------
+    fx_bf16x8 bh[4], bl[4];
+    float al1;
+    {
+        const float4 *src = reinterpret_cast<const float4 *>(fl + ((size_t)y * W + (xok ? x : 0)) * 64);
+        float4 lraw[8];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            lraw[2 * s] = src[4 * s + 2 * h];
+            lraw[2 * s + 1] = src[4 * s + 2 * h + 1];
+        }
+        float q1 = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const float e[8] = {lraw[2 * s].x, lraw[2 * s].y, lraw[2 * s].z, lraw[2 * s].w,
+                                lraw[2 * s + 1].x, lraw[2 * s + 1].y, lraw[2 * s + 1].z, lraw[2 * s + 1].w};
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                __bf16 hh, ll;
+                fx_split(e[i], hh, ll);
+                bh[s][i] = hh;
+                bl[s][i] = ll;
+                q1 += fabsf(e[i]);
+            }
+        }
+        al1 = q1 + __shfl_xor(q1, 32, 64);
+    }
+
+    float b1[4], b2[4];
+    int ag[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) { b1[t] = -__builtin_inff(); b2[t] = -__builtin_inff(); ag[t] = -1; }
+
+    for (int dc0 = d0; dc0 < d1; dc0 += FX_DCH) {
+        const int dc1 = min(dc0 + FX_DCH, d1);
+        const int nt = (dc1 - dc0 + 63 + 31) / 32;
+        const int rb = x0 + FX_NX - dc0 - 32 * nt;     // right pixel of window row 0
+        const int niter = nt * 2;                      // nt*32 pixels * 16 float4 / 256 threads
+        float4 rraw[2 * FX_NT];
+#pragma unroll
+        for (int k = 0; k < 2 * FX_NT; k++) {
+            const int idx = k * 256 + tid;
+            const int xr = min(max(rb + (idx >> 4), 0), W - 1);
+            rraw[k] = frow[(size_t)xr * 16 + (idx & 15)];
+        }
+        __syncthreads();   // previous chunk's plane reads are done
+        float binf = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 2 * FX_NT; k++) {
+            if (k >= niter) continue;   // wave-uniform; rraw[] stays statically indexed
+            const int idx = k * 256 + tid;
+            const int px = idx >> 4, q = idx & 15;
+            const int xr = rb + px;
+            const float4 v = (xr >= 0 && xr < W) ? rraw[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            binf = fmaxf(binf, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            __bf16 h0, h1, h2, h3, l0, l1, l2, l3;
+            fx_split(v.x, h0, l0); fx_split(v.y, h1, l1); fx_split(v.z, h2, l2); fx_split(v.w, h3, l3);
+            typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+            const bf4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+            const int sl = fx_slot(px, q >> 1);
+            reinterpret_cast<uint2 *>(pl_hi + sl)[q & 1] = __builtin_bit_cast(uint2, hv);
+            reinterpret_cast<uint2 *>(pl_lo + sl)[q & 1] = __builtin_bit_cast(uint2, lv);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) binf = fmaxf(binf, __shfl_xor(binf, o, 64));
+        if (lane == 0) atomicMax(&binf_bits, __float_as_uint(binf));   // non-negative: uint order
+        __syncthreads();
+
+        // ---- MFMA tiles: wave owns N-tile n, M-tiles m = mpar, mpar+2, ... ----
+        const int xbase = x0 + 32 * n;
+        for (int m = mpar; m < nt; m += 2) {
+            const int dt = xbase - (rb + 32 * m);
+            const int dlo = dt - 31, dhi = dt + 31;
+            if (dhi < dc0 || dlo >= dc1) continue;     // wave-uniform
+            fx_floatx16 acc = {0};
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int sl = fx_slot(32 * m + j, 2 * s + h);
+                const fx_bf16x8 ah = __builtin_bit_cast(fx_bf16x8, pl_hi[sl]);
+                const fx_bf16x8 al = __builtin_bit_cast(fx_bf16x8, pl_lo[sl]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+            }
+            const int dl = dt + j - 4 * h;             // d of register r is dl - ((r&3) + 8(r>>2))
+            const bool interior = (dlo >= dc0) && (dhi < dc1);
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int t = r & 3;
+                const int d = dl - ((r & 3) + 8 * (r >> 2));
+                float sc = acc[r];
+                if (!interior) sc = (d >= dc0 && d < dc1) ? sc : -__builtin_inff();
+                const bool gt = sc > b1[t];
+                ag[t] = gt ? d : ag[t];
+                b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                b1[t] = fmaxf(b1[t], sc);
+            }
+        }
+    }
+
+    // ---- merge states, lane pair, waves; certify ---------------------------
+    float best = b1[0], second = b2[0];
+    int arg = ag[0];
+#pragma unroll
+    for (int t = 1; t < 4; t++) fx_merge(best, arg, second, b1[t], ag[t], b2[t]);
+    {
+        const float bb = __shfl_xor(best, 32, 64), ss = __shfl_xor(second, 32, 64);
+        const int aa = __shfl_xor(arg, 32, 64);
+        fx_merge(best, arg, second, bb, aa, ss);
+    }
+    mb[wave][lane] = best;
+    ma[wave][lane] = arg;
+    ms[wave][lane] = second;
+    __syncthreads();
+    if (wave < 2 && h == 0 && xok) {
+        fx_merge(best, arg, second, mb[wave + 2][lane], ma[wave + 2][lane], ms[wave + 2][lane]);
+        const float eps = FX_K * al1 * __uint_as_float(binf_bits) + FX_ABS;
+        const size_t p = (size_t)y * W + x;
+        if ((best - second) > 2.0f * eps && arg >= 0) {
+            if (out_min) {
+                float cost = -0.0f;
+                if (x - arg >= 0)   // exact cost of the winner: NumPy pairwise order, as cv64_kernel
+                    cost = dot64_exact_global(reinterpret_cast<const float4 *>(fl + p * 64),
+                                              reinterpret_cast<const float4 *>(fr + (p - arg) * 64));
+                out_min[p] = cost;
+            }
+            if (out_arg) out_arg[p] = arg;
+            if (out_disp) out_disp[p] = (float)arg;
+        } else {
+            const unsigned e = atomicAdd(counter, 1u);
+            list[e] = (int32_t)p;
+        }
+    }
+}
+
+// Exact resolution of the listed pixels: one wave per pixel, lanes split the
+// d range (increasing d per lane), then a (value, index) merge == sequential scan.
+__global__ __launch_bounds__(256) void cv_wta_fixup_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                           int W, int d0, int d1, const unsigned *__restrict__ counter,
+                                                           const int32_t *__restrict__ list, float *__restrict__ out_min,
+                                                           int32_t *__restrict__ out_arg, float *__restrict__ out_disp)
+{
+    const unsigned cnt = *counter;
+    const int lane = threadIdx.x & 63;
+    const unsigned nw = gridDim.x * 4;
+    for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < cnt; e += nw) {
+        const size_t p = (size_t)list[e];
+        const int x = (int)(p % W);
+        const size_t rowbase = p - x;
+        const float4 *a = reinterpret_cast<const float4 *>(fl + p * 64);
+        float best = __builtin_inff();
+        int arg = -1;
+        for (int d = d0 + lane; d < d1; d += 64) {
+            float cost = -0.0f;
+            if (x >= d) cost = dot64_exact_global(a, reinterpret_cast<const float4 *>(fr + (rowbase + x - d) * 64));
+            if (cost < best) { best = cost; arg = d; }
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float ob = __shfl_xor(best, off, 64);
+            const int oa = __shfl_xor(arg, off, 64);
+            argmin_merge(best, arg, ob, oa);
+        }
+        if (lane == 0) {
+            if (out_min) out_min[p] = best;
+            if (out_arg) out_arg[p] = arg;
+            if (out_disp) out_disp[p] = (float)arg;
+        }
+    }
+}
+
 }  // namespace sde
 
 using namespace sde;
@@ -301,13 +586,29 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
     return launch_status();
 }
 
+SDE_EXPORT int64_t sde_cv_wta_workspace_bytes(int H, int W)
+{
+    if (H <= 0 || W <= 0) return -1;
+    return 256 + 4 * (int64_t)H * W;
+}
+
 SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, int d1, float *disp,
-                          float *min_cost, int32_t *argmin, void *stream)
+                          float *min_cost, int32_t *argmin, int mode, void *workspace, int64_t workspace_bytes,
+                          void *stream)
 {
     if (!fl || !fr || H <= 0 || W <= 0 || C <= 0 || d0 < 0 || d1 <= d0) return SDE_ERR_ARG;
     if (!disp && !min_cost && !argmin) return SDE_ERR_ARG;
+    if (mode != SDE_CV_EXACT && mode != SDE_CV_CERTIFIED) return SDE_ERR_ARG;
     hipStream_t st = as_stream(stream);
-    if (C == 64) {
+    if (C == 64 && mode == SDE_CV_CERTIFIED) {
+        if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
+        unsigned *counter = reinterpret_cast<unsigned *>(workspace);
+        int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
+        if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+        cv_wta_fast_kernel<<<cdiv(W, FX_NX) * H, 256, 0, st>>>(fl, fr, H, W, d0, d1, min_cost, argmin, disp, counter,
+                                                               list);
+        cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
+    } else if (C == 64) {
         dim3 grid(cdiv(W, CV_TX), H);
         cv64_kernel<SDE_SIDE_LEFT, OUT_WTA><<<grid, 256, 0, st>>>(fl, fr, H, W, d0, d1, 0, -0.0f, nullptr,
                                                                    min_cost, argmin, disp);

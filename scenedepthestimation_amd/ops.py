@@ -79,8 +79,21 @@ def cost_volume(fl, fr, ndisp: int, layout: str = "DHW", right: bool = False, in
     return (out_left, out_right) if right else out_left
 
 
-def cv_wta(fl, fr, d0: int, d1: int, disp=None, min_cost=None, argmin=None, want=("disp",)):
-    """Fused cost volume + first-min over [d0, d1): WTA1(compute_cost_volume(fl, fr, d1)) when d0 = 0."""
+CV_MODES = {"exact": _lib.SDE_CV_EXACT, "certified": _lib.SDE_CV_CERTIFIED}
+
+
+def cv_wta_workspace_bytes(H: int, W: int) -> int:
+    return int(lib.sde_cv_wta_workspace_bytes(H, W))
+
+
+def cv_wta(fl, fr, d0: int, d1: int, disp=None, min_cost=None, argmin=None, want=("disp",), mode: str = "certified",
+           workspace=None):
+    """Fused cost volume + first-min over [d0, d1): WTA1(compute_cost_volume(fl, fr, d1)) when d0 = 0.
+
+    mode 'exact' (VALU, NumPy order for every voxel) or 'certified' (bf16x3 MFMA scores + error bound,
+    exact resolution of uncertified pixels): identical outputs.  workspace: uint8 tensor of
+    cv_wta_workspace_bytes(H, W) bytes (allocated if None); its first int32 holds the number of
+    pixels resolved exactly after the call."""
     pl, pr, H, W, C = _feat_pair(fl, fr)
     if "disp" in want and disp is None:
         disp = _empty((H, W), torch.float32, fl)
@@ -91,8 +104,20 @@ def cv_wta(fl, fr, d0: int, d1: int, disp=None, min_cost=None, argmin=None, want
     pd = _need(disp, "disp", shape=(H, W)) if disp is not None else None
     pm = _need(min_cost, "min_cost", shape=(H, W)) if min_cost is not None else None
     pa = _need(argmin, "argmin", dtype=torch.int32, shape=(H, W)) if argmin is not None else None
-    check(lib.sde_cv_wta(pl, pr, H, W, C, int(d0), int(d1), pd, pm, pa, _stream()), "sde_cv_wta")
+    md = CV_MODES[mode]
+    pws, wsb = None, 0
+    if md == _lib.SDE_CV_CERTIFIED:
+        need = cv_wta_workspace_bytes(H, W)
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.uint8, device=fl.device)
+        pws, wsb = _need(workspace, "workspace", dtype=torch.uint8), workspace.numel()
+    check(lib.sde_cv_wta(pl, pr, H, W, C, int(d0), int(d1), pd, pm, pa, md, pws, wsb, _stream()), "sde_cv_wta")
     return disp, min_cost, argmin
+
+
+def cv_wta_fixups(workspace) -> int:
+    """Number of pixels the last certified cv_wta call resolved with the exact scan (synchronises)."""
+    return int(workspace[:4].view(torch.int32).item())
 
 
 def wta(vol, layout: str = "DHW", rule: str = "inf", out=None):

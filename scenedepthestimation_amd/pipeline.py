@@ -24,7 +24,8 @@ from . import mc_cnn, ops
 
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
-                 nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6"):
+                 nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6",
+                 cv_mode: str = "certified"):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)
         self.nlayers, self.nf = int(nlayers), int(nf)
         if tower_precision not in ops.TOWER_PRECISIONS:
@@ -47,6 +48,8 @@ class StereoMatcher:
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
         self.min_cost = torch.empty((H, W), dtype=torch.float32, device=dev)
         self.argmin = torch.empty((H, W), dtype=torch.int32, device=dev)
+        self.cv_mode = cv_mode
+        self.cv_ws = torch.empty(ops.cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device=dev)
         self.sgm_bufs = None
         if sgm:
             self._alloc_sgm()
@@ -78,7 +81,8 @@ class StereoMatcher:
         return ops.cv_wta(self.feat[0], self.feat[1], self.d0, self.d1,
                           disp=self.disp if "disp" in want else None,
                           min_cost=self.min_cost if "min" in want else None,
-                          argmin=self.argmin if "argmin" in want else None, want=())
+                          argmin=self.argmin if "argmin" in want else None, want=(),
+                          mode=self.cv_mode, workspace=self.cv_ws)
 
     def match(self):
         """One pass of the hot path on the resident images: features + fused CV/WTA -> disparity."""

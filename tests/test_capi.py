@@ -65,7 +65,9 @@ def test_argument_validation_without_gpu():
     ERR = -1
     assert lib.sde_cost_volume(None, None, 4, 4, 64, 4, 0, 1, ctypes.c_float(0.0), None, None, None) == ERR
     assert lib.sde_cost_volume(1, 1, 4, 4, 64, 4, 0, 2, ctypes.c_float(0.0), 1, 1, None) == ERR   # right needs HWD
-    assert lib.sde_cv_wta(1, 1, 4, 4, 64, 5, 5, 1, None, None, None) == ERR                        # empty shard
+    assert lib.sde_cv_wta(1, 1, 4, 4, 64, 5, 5, 1, None, None, 0, None, 0, None) == ERR           # empty shard
+    assert lib.sde_cv_wta(1, 1, 4, 4, 64, 0, 5, 1, None, None, 1, None, 0, None) == -3            # workspace
+    assert lib.sde_cv_wta(1, 1, 4, 4, 64, 0, 5, 1, None, None, 7, None, 0, None) == ERR           # mode
     assert lib.sde_wta(1, 4, 4, 4, 7, 0, 1, None) == ERR                                            # bad layout
     assert lib.sde_sgm_8path(1, 1, 1, 5, 8, 1, None) == ERR                                        # H < 2
     assert lib.sde_sgm_8path(1, 1, 5, 5, 513, 1, None) == ERR                                      # D > 512

@@ -102,7 +102,8 @@ def test_disparity_shards_merge_bit_exact(gpu, oracle, nshards):
     args = torch.empty((nshards, H, W), dtype=torch.int32, device="cuda")
     for s in range(nshards):
         d0, d1 = shard_range(D, nshards, s)
-        ops.cv_wta(dev(fl), dev(fr), d0, d1, min_cost=mins[s], argmin=args[s], want=())
+        ops.cv_wta(dev(fl), dev(fr), d0, d1, min_cost=mins[s], argmin=args[s], want=(),
+                   mode="certified" if s % 2 else "exact")
     assert np.array_equal(host(ops.argmin_merge(mins, args)), ref)
 
 
@@ -297,3 +298,74 @@ def test_cli_match_single_end_to_end(gpu, tmp_path, monkeypatch):
     assert out.shape == (48, 96) and out.max() < 16
     match_single.main(["-i", "3", "-g", "0", "--checkpoint", "synthetic", "--ndisp", "16", "-f", "sgm"])
     assert imageio.imread_gray(str(tmp_path / "result" / "sgm" / "ld3.png")).shape == (48, 96)
+
+
+# ----------------------------------------------------------------------------
+# certified fast path: bit-identical to the exact kernel for every input
+# ----------------------------------------------------------------------------
+def _both_modes(fl, fr, d0, d1):
+    from scenedepthestimation_amd import ops
+    outs = {}
+    for mode in ("exact", "certified"):
+        ws = torch.empty(ops.cv_wta_workspace_bytes(*fl.shape[:2]), dtype=torch.uint8, device="cuda")
+        disp, mn, am = ops.cv_wta(dev(fl), dev(fr), d0, d1, want=("disp", "min", "argmin"), mode=mode, workspace=ws)
+        outs[mode] = (host(disp), host(mn), host(am), ops.cv_wta_fixups(ws) if mode == "certified" else 0)
+    return outs
+
+
+def test_certified_golden(gpu, golden, golden_cases):
+    from scenedepthestimation_amd import ops
+    for n in golden_cases:
+        fl, fr, d = golden[n + "__fl"], golden[n + "__fr"], int(golden[n + "__ndisp"])
+        disp, _, _ = ops.cv_wta(dev(fl), dev(fr), 0, d, mode="certified")
+        assert np.array_equal(host(disp), golden[n + "__disp"]), n
+
+
+@pytest.mark.parametrize("H,W,D,d0", [(3, 200, 64, 0), (2, 333, 192, 0), (2, 130, 256, 0), (2, 700, 512, 0),
+                                      (3, 97, 100, 0), (2, 300, 192, 40), (2, 64, 192, 0), (1, 5, 9, 0)])
+def test_certified_matches_exact(gpu, oracle, H, W, D, d0):
+    rng = np.random.default_rng(H * 1000 + W + D)
+    fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    o = _both_modes(fl, fr, d0, D)
+    for k in range(3):
+        assert o["exact"][k].tobytes() == o["certified"][k].tobytes(), k
+    omn, oam = oracle.cv_wta_shard(fl, fr, d0, D)
+    assert np.array_equal(o["certified"][2], oam) and o["certified"][1].tobytes() == omn.tobytes()
+
+
+def test_certified_adversarial_ties_and_nonfinite(gpu, oracle):
+    rng = np.random.default_rng(123)
+    H, W, D = 4, 260, 96
+    fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    fr[0] = fr[0, 7]                       # a constant row: every valid d ties exactly
+    fr[1, 100:160] = fr[1, 40:100]         # periodic texture: exact ties at two disparities
+    fr[2, :, :32] *= 1.0 + 1e-6            # near-ties below the fast path's resolution
+    fl[3, 50] = np.inf                     # non-finite features take the exact path
+    fr[3, 10] = np.nan
+    fl[3, 200] = 0.0                       # zero vector: all costs -0.0
+    o = _both_modes(fl, fr, 0, D)
+    for k in range(3):
+        assert o["exact"][k].tobytes() == o["certified"][k].tobytes(), k
+    assert o["certified"][3] >= W          # the constant row alone needs the exact scan
+    ref = oracle.WTA1(oracle.compute_cost_volume(np.nan_to_num(fl[:3]), fr[:3], D))
+    assert np.array_equal(o["certified"][0][:3], ref)
+
+
+def test_certified_fixup_rate_is_small_on_textured_pairs(gpu):
+    """On a textured synthetic pair through the real tower, almost every pixel is certified."""
+    from scenedepthestimation_amd import ops
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    H, W, D = 128, 256, 64
+    left, right, _ = stereo_pair(H, W, D, seed=4)
+    m = StereoMatcher(H, W, D)
+    m.load_images(left, right)
+    m.features()
+    m.cost_wta()
+    fix = ops.cv_wta_fixups(m.cv_ws)
+    exact, _, _ = ops.cv_wta(m.feat[0], m.feat[1], 0, D, mode="exact")
+    assert np.array_equal(host(m.disp), host(exact))
+    print("certified fix-up pixels:", fix, "of", H * W)
+    assert fix < 0.2 * H * W
