@@ -104,13 +104,15 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
                 o = acts[cur ^ 1].view(-1)[: (hin - 2) * (win - 2) * NF].view(hin - 2, win - 2, NF)
             src = acts[cur].view(-1)[: hin * win * NF].view(hin, win, NF)
             e = t_conv.start() if (timed and layer == 3) else None
-            ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision)
+            ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision,
+                            split=m.split[i] if (layer == L and m.split) else None)
             if e is not None:
                 t_conv.stop(e)
             hin, win = hin - 2, win - 2
             cur ^= 1
         if e_t is not None:
             t_tower.stop(e_t)
+        m.split_valid = m.split is not None
 
     def step(timed=False):
         if what == "tower+cv_wta":

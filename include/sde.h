@@ -101,6 +101,27 @@ int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, in
                void *stream);
 
 /*
+ * Split a [npix][64] float32 feature map for SDE_CV_CERTIFIED: hi = bf16_rne(x),
+ * lo = bf16_rne(x - hi) (both [npix][64] bf16 bit patterns) and norm[p] >= the
+ * pixel's L2 norm.  The tower can emit the same three outputs from its last
+ * layer (sde_tower_forward's feat_hi / feat_lo / feat_norm).
+ */
+int sde_feature_split(const float *feat, int64_t npix, int C, uint16_t *hi, uint16_t *lo, float *norm, void *stream);
+
+/* Workspace bytes for sde_cv_wta_split (work-list of unresolved pixels). */
+int64_t sde_cv_wta_split_workspace_bytes(int H, int W);
+
+/*
+ * SDE_CV_CERTIFIED on pre-split operands (no split pass): same outputs and
+ * bit-exactness as sde_cv_wta.  fl / fr (float32) are read only for the exact
+ * resolution of uncertified pixels and for min_cost.
+ */
+int sde_cv_wta_split(const float *fl, const float *fr, const uint16_t *fl_hi, const uint16_t *fl_lo,
+                     const float *fl_norm, const uint16_t *fr_hi, const uint16_t *fr_lo, const float *fr_norm,
+                     int H, int W, int d0, int d1, float *disp, float *min_cost, int32_t *argmin, void *workspace,
+                     int64_t workspace_bytes, void *stream);
+
+/*
  * Ordered merge of per-shard (min, argmin) pairs: shard s covers a disparity
  * range that precedes shard s+1's; strict `<` keeps the earliest on ties.
  * mins/args: [nshards][npix].  disp: float32 [npix].
@@ -136,9 +157,13 @@ int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf);
  * img_pad: float32 [(H+2*nlayers)][(W+2*nlayers)] zero-padded normalised image
  * (process_functional.py:13-19).  feat: float32 [H][W][nf], L2-normalised per
  * pixel (mc_cnn_brunch.py:48).  packed: device copy of the packed weights.
+ * feat_hi / feat_lo / feat_norm (optional, NULL to skip; nlayers >= 2): the
+ * last layer's epilogue also writes the bf16 split planes and per-pixel norm
+ * bound that sde_cv_wta_split consumes (same layout as sde_feature_split).
  */
 int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
-                      float *feat, void *workspace, int64_t workspace_bytes, int flags, void *stream);
+                      float *feat, void *workspace, int64_t workspace_bytes, int flags, uint16_t *feat_hi,
+                      uint16_t *feat_lo, float *feat_norm, void *stream);
 
 /*
  * One layer of the tower as a single kernel launch (for per-layer timing and
@@ -147,7 +172,7 @@ int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, i
  * nf activations, out (Hin-2) x (Win-2) x nf.  Layer nlayers L2-normalises.
  */
 int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
-                    float *out, int flags, void *stream);
+                    float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm, void *stream);
 
 /*
  * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):

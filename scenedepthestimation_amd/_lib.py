@@ -37,14 +37,19 @@ SIGNATURES = {
     "sde_cv_wta_workspace_bytes": (c_int64, [c_int, c_int]),
     "sde_cv_wta": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                            c_void_p, c_int, c_void_p, c_int64, c_void_p]),
+    "sde_feature_split": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sde_cv_wta_split_workspace_bytes": (c_int64, [c_int, c_int]),
+    "sde_cv_wta_split": (c_int, [c_void_p] * 8 + [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                 c_int64, c_void_p]),
     "sde_argmin_merge": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "sde_tower_packed_floats": (c_int64, [c_int, c_int]),
     "sde_tower_pack_weights": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int,
                                        c_void_p]),
     "sde_tower_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
     "sde_tower_forward": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                  c_int64, c_int, c_void_p]),
-    "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+                                  c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                c_void_p, c_void_p, c_void_p]),
     "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
                                   c_void_p]),

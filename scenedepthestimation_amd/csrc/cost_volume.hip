@@ -325,30 +325,55 @@ __device__ __forceinline__ int xcd_remap(int b, int nb)
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// One workgroup per (row, 64-pixel strip); 3 workgroups per CU (<= 168 VGPRs,
-// 50 KB LDS) hide each other's memory latency.  Every global load of a
-// workgroup is issued up front from clamped addresses (no per-element
-// branches), so a workgroup pays about one memory round trip.
-//
-// Error bound per pixel: sum_c |a_c b_c| <= ||a||_1 * max_window |b|, so
-// eps = FX_K * ||fl[x]||_1 * ||fr window||_inf + FX_ABS needs no cross-lane
-// norm reductions while staging.
-//
-// Top-2 tracking per lane in 4 independent states (register r -> state r&3)
-// for ILP: best' = max(best, v), second' = med3(best, second, v) (best >=
-// second), arg' = v > best ? d : arg.
-__global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
-                                                             int H, int W, int d0, int d1,
-                                                             float *__restrict__ out_min, int32_t *__restrict__ out_arg,
-                                                             float *__restrict__ out_disp, unsigned *__restrict__ counter,
-                                                             int32_t *__restrict__ list)
+// Split of a feature map for the certified path: x = hi + lo + r with hi =
+// bf16_rne(x), lo = bf16_rne(x - hi) (|r| <= 2^-16 |x|), plus an upper bound of
+// each pixel's L2 norm (fp32 sum of 64 squares, relative error <= 64*2^-24,
+// inflated by (1 + 4e-6)).  16 lanes per pixel, one float4 each.
+constexpr float FX_NORM_UP = 1.000004f;
+
+__global__ __launch_bounds__(256) void feature_split_kernel(const float *__restrict__ f, int64_t npix,
+                                                            uint16_t *__restrict__ hi, uint16_t *__restrict__ lo,
+                                                            float *__restrict__ nrm)
 {
-    __shared__ uint4 pl_hi[FX_WIN * 8];
-    __shared__ uint4 pl_lo[FX_WIN * 8];
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = idx < npix * 16;
+    const float4 v = ok ? reinterpret_cast<const float4 *>(f)[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    ss += __shfl_xor(ss, 4, 64);
+    ss += __shfl_xor(ss, 8, 64);
+    if (!ok) return;
+    __bf16 h0, h1, h2, h3, l0, l1, l2, l3;
+    fx_split(v.x, h0, l0); fx_split(v.y, h1, l1); fx_split(v.z, h2, l2); fx_split(v.w, h3, l3);
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const bf4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+    reinterpret_cast<uint2 *>(hi)[idx] = __builtin_bit_cast(uint2, hv);
+    reinterpret_cast<uint2 *>(lo)[idx] = __builtin_bit_cast(uint2, lv);
+    if ((idx & 15) == 0) nrm[idx >> 4] = sqrtf(ss) * FX_NORM_UP;
+}
+
+// Certified fast kernel on pre-split operands.  One workgroup per (row,
+// 64-pixel strip), <= 128-disparity chunks (window <= 6 M-tiles = 192 pixels,
+// 48 KB of hi/lo planes in LDS -> 3 workgroups per CU).  The window is staged
+// by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no VALU): each wave-instruction
+// fills 1 KB of the swizzled image linearly, so the swizzle is applied to the
+// per-lane SOURCE chunk.  Invalid voxels (x - d < 0: exact cost -0.0) are
+// forced to score +0 in the edge-tile path.
+__global__ __launch_bounds__(256) void cv_wta_cert_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                          const uint4 *__restrict__ lhi, const uint4 *__restrict__ llo,
+                                                          const float *__restrict__ lnrm,
+                                                          const uint4 *__restrict__ rhi, const uint4 *__restrict__ rlo,
+                                                          const float *__restrict__ rnrm, int H, int W, int d0, int d1,
+                                                          float *__restrict__ out_min, int32_t *__restrict__ out_arg,
+                                                          float *__restrict__ out_disp, unsigned *__restrict__ counter,
+                                                          int32_t *__restrict__ list)
+{
+    __shared__ uint4 pl[2 * FX_WIN * 8];            // [plane][pixel][8 chunks], swizzled
     __shared__ float mb[4][64];
     __shared__ int ma[4][64];
     __shared__ float ms[4][64];
-    __shared__ unsigned binf_bits;
+    __shared__ unsigned nmax_bits;
 
     const int nbx = (W + FX_NX - 1) / FX_NX;
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -359,37 +384,20 @@ __global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__rest
     const int j = lane & 31, h = lane >> 5;
     const int x = x0 + 32 * n + j;
     const bool xok = x < W;
-    const float4 *frow = reinterpret_cast<const float4 *>(fr + (size_t)y * W * 64);
+    const size_t rowpix = (size_t)y * W;
+    if (tid == 0) nmax_bits = 0u;
 
-    if (tid == 0) binf_bits = 0u;
-
-    // ---- left operand (8 float4 per lane), split hi/lo; ||a||_1 ------------
+    // left operand: 16-B chunks 2s+h of this lane's pixel (channels 16s+8h..+7)
     fx_bf16x8 bh[4], bl[4];
-    float al1;
     {
-        const float4 *src = reinterpret_cast<const float4 *>(fl + ((size_t)y * W + (xok ? x : 0)) * 64);
-        float4 lraw[8];
+        const size_t pc = (rowpix + (xok ? x : 0)) * 8;
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            lraw[2 * s] = src[4 * s + 2 * h];
-            lraw[2 * s + 1] = src[4 * s + 2 * h + 1];
+            bh[s] = __builtin_bit_cast(fx_bf16x8, lhi[pc + 2 * s + h]);
+            bl[s] = __builtin_bit_cast(fx_bf16x8, llo[pc + 2 * s + h]);
         }
-        float q1 = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const float e[8] = {lraw[2 * s].x, lraw[2 * s].y, lraw[2 * s].z, lraw[2 * s].w,
-                                lraw[2 * s + 1].x, lraw[2 * s + 1].y, lraw[2 * s + 1].z, lraw[2 * s + 1].w};
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                __bf16 hh, ll;
-                fx_split(e[i], hh, ll);
-                bh[s][i] = hh;
-                bl[s][i] = ll;
-                q1 += fabsf(e[i]);
-            }
-        }
-        al1 = q1 + __shfl_xor(q1, 32, 64);
     }
+    const float nl = lnrm[rowpix + (xok ? x : 0)];
 
     float b1[4], b2[4];
     int ag[4];
@@ -400,38 +408,34 @@ __global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__rest
         const int dc1 = min(dc0 + FX_DCH, d1);
         const int nt = (dc1 - dc0 + 63 + 31) / 32;
         const int rb = x0 + FX_NX - dc0 - 32 * nt;     // right pixel of window row 0
-        const int niter = nt * 2;                      // nt*32 pixels * 16 float4 / 256 threads
-        float4 rraw[2 * FX_NT];
-#pragma unroll
-        for (int k = 0; k < 2 * FX_NT; k++) {
-            const int idx = k * 256 + tid;
-            const int xr = min(max(rb + (idx >> 4), 0), W - 1);
-            rraw[k] = frow[(size_t)xr * 16 + (idx & 15)];
+        __syncthreads();                               // previous chunk's plane reads are done
+        // LDS-DMA: 2 planes x nt*32 pixels x 8 chunks = nt*8 KB; 1 KB (8 pixels) per wave-instruction
+        const int ninst = nt * 4 * 2;                  // per plane nt*4 instructions
+        for (int ii = wave; ii < ninst; ii += 4) {
+            const int plane = ii / (nt * 4);
+            const int slot = (ii - plane * nt * 4) * 64 + lane;   // 16-B slot within the plane image
+            const int r = slot >> 3, cs = slot & 7;
+            const int c8 = cs ^ ((r >> 1) & 7);                  // source chunk for this LDS slot
+            const int xr = min(max(rb + r, 0), W - 1);
+            const uint4 *src = (plane ? rlo : rhi) + (rowpix + xr) * 8 + c8;
+            __builtin_amdgcn_global_load_lds((const void *)src,
+                                             (__attribute__((address_space(3))) void *)(pl + plane * FX_WIN * 8 +
+                                                                                        (ii - plane * nt * 4) * 64),
+                                             16, 0, 0);
         }
-        __syncthreads();   // previous chunk's plane reads are done
-        float binf = 0.0f;
+        // window norm bound: max over its pixels
+        {
+            float nm = 0.0f;
+            for (int r = tid; r < nt * 32; r += 256) {
+                const int xr = rb + r;
+                if (xr >= 0 && xr < W) nm = fmaxf(nm, rnrm[rowpix + xr]);
+            }
 #pragma unroll
-        for (int k = 0; k < 2 * FX_NT; k++) {
-            if (k >= niter) continue;   // wave-uniform; rraw[] stays statically indexed
-            const int idx = k * 256 + tid;
-            const int px = idx >> 4, q = idx & 15;
-            const int xr = rb + px;
-            const float4 v = (xr >= 0 && xr < W) ? rraw[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-            binf = fmaxf(binf, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-            __bf16 h0, h1, h2, h3, l0, l1, l2, l3;
-            fx_split(v.x, h0, l0); fx_split(v.y, h1, l1); fx_split(v.z, h2, l2); fx_split(v.w, h3, l3);
-            typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-            const bf4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
-            const int sl = fx_slot(px, q >> 1);
-            reinterpret_cast<uint2 *>(pl_hi + sl)[q & 1] = __builtin_bit_cast(uint2, hv);
-            reinterpret_cast<uint2 *>(pl_lo + sl)[q & 1] = __builtin_bit_cast(uint2, lv);
+            for (int o = 1; o < 64; o <<= 1) nm = fmaxf(nm, __shfl_xor(nm, o, 64));
+            if (lane == 0) atomicMax(&nmax_bits, __float_as_uint(nm));   // non-negative: uint order
         }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) binf = fmaxf(binf, __shfl_xor(binf, o, 64));
-        if (lane == 0) atomicMax(&binf_bits, __float_as_uint(binf));   // non-negative: uint order
-        __syncthreads();
+        __syncthreads();                               // drains the DMA (vmcnt(0)) and publishes it
 
-        // ---- MFMA tiles: wave owns N-tile n, M-tiles m = mpar, mpar+2, ... ----
         const int xbase = x0 + 32 * n;
         for (int m = mpar; m < nt; m += 2) {
             const int dt = xbase - (rb + 32 * m);
@@ -441,29 +445,42 @@ __global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__rest
 #pragma unroll
             for (int s = 0; s < 4; s++) {
                 const int sl = fx_slot(32 * m + j, 2 * s + h);
-                const fx_bf16x8 ah = __builtin_bit_cast(fx_bf16x8, pl_hi[sl]);
-                const fx_bf16x8 al = __builtin_bit_cast(fx_bf16x8, pl_lo[sl]);
+                const fx_bf16x8 ah = __builtin_bit_cast(fx_bf16x8, pl[sl]);
+                const fx_bf16x8 al = __builtin_bit_cast(fx_bf16x8, pl[FX_WIN * 8 + sl]);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
             }
             const int dl = dt + j - 4 * h;             // d of register r is dl - ((r&3) + 8(r>>2))
-            const bool interior = (dlo >= dc0) && (dhi < dc1);
+            const int xrl = rb + 32 * m + 4 * h;       // right pixel of register r is xrl + ((r&3) + 8(r>>2))
+            if (dlo >= dc0 && dhi < dc1 && rb + 32 * m >= 0) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int t = r & 3;
-                const int d = dl - ((r & 3) + 8 * (r >> 2));
-                float sc = acc[r];
-                if (!interior) sc = (d >= dc0 && d < dc1) ? sc : -__builtin_inff();
-                const bool gt = sc > b1[t];
-                ag[t] = gt ? d : ag[t];
-                b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
-                b1[t] = fmaxf(b1[t], sc);
+                for (int r = 0; r < 16; r++) {
+                    const int t = r & 3;
+                    const int d = dl - ((r & 3) + 8 * (r >> 2));
+                    const float sc = acc[r];
+                    const bool gt = sc > b1[t];
+                    ag[t] = gt ? d : ag[t];
+                    b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                    b1[t] = fmaxf(b1[t], sc);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int t = r & 3;
+                    const int ri = (r & 3) + 8 * (r >> 2);
+                    const int d = dl - ri;
+                    float sc = (xrl + ri < 0) ? 0.0f : acc[r];          // x < d: exact cost -0.0
+                    sc = (d >= dc0 && d < dc1) ? sc : -__builtin_inff();
+                    const bool gt = sc > b1[t];
+                    ag[t] = gt ? d : ag[t];
+                    b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                    b1[t] = fmaxf(b1[t], sc);
+                }
             }
         }
     }
 
-    // ---- merge states, lane pair, waves; certify ---------------------------
     float best = b1[0], second = b2[0];
     int arg = ag[0];
 #pragma unroll
@@ -479,8 +496,8 @@ __global__ __launch_bounds__(256, 3) void cv_wta_fast_kernel(const float *__rest
     __syncthreads();
     if (wave < 2 && h == 0 && xok) {
         fx_merge(best, arg, second, mb[wave + 2][lane], ma[wave + 2][lane], ms[wave + 2][lane]);
-        const float eps = FX_K * al1 * __uint_as_float(binf_bits) + FX_ABS;
-        const size_t p = (size_t)y * W + x;
+        const float eps = FX_K * nl * __uint_as_float(nmax_bits) + FX_ABS;
+        const size_t p = rowpix + x;
         if ((best - second) > 2.0f * eps && arg >= 0) {
             if (out_min) {
                 float cost = -0.0f;
@@ -586,10 +603,62 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
     return launch_status();
 }
 
+// certified-mode workspace: [counter 256 B][list 4*npix][planes 4 x 128*npix][norms 2 x 4*npix]
+static int64_t cert_ws_bytes(int H, int W, bool with_planes)
+{
+    const int64_t npix = (int64_t)H * W;
+    int64_t b = 256 + ((4 * npix + 255) / 256) * 256;
+    if (with_planes) b += 4 * 128 * npix + 2 * ((4 * npix + 255) / 256) * 256;
+    return b;
+}
+
 SDE_EXPORT int64_t sde_cv_wta_workspace_bytes(int H, int W)
 {
     if (H <= 0 || W <= 0) return -1;
-    return 256 + 4 * (int64_t)H * W;
+    return cert_ws_bytes(H, W, true);
+}
+
+SDE_EXPORT int sde_feature_split(const float *feat, int64_t npix, int C, uint16_t *hi, uint16_t *lo, float *norm,
+                                 void *stream)
+{
+    if (!feat || !hi || !lo || !norm || npix <= 0 || C != 64) return SDE_ERR_ARG;
+    feature_split_kernel<<<cdiv(npix * 16, 256), 256, 0, as_stream(stream)>>>(feat, npix, hi, lo, norm);
+    return launch_status();
+}
+
+static int launch_cert(const float *fl, const float *fr, const uint16_t *lhi, const uint16_t *llo, const float *lnrm,
+                       const uint16_t *rhi, const uint16_t *rlo, const float *rnrm, int H, int W, int d0, int d1,
+                       float *disp, float *min_cost, int32_t *argmin, void *ws, hipStream_t st)
+{
+    unsigned *counter = reinterpret_cast<unsigned *>(ws);
+    int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + 256);
+    if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+    cv_wta_cert_kernel<<<cdiv(W, FX_NX) * H, 256, 0, st>>>(
+        fl, fr, reinterpret_cast<const uint4 *>(lhi), reinterpret_cast<const uint4 *>(llo), lnrm,
+        reinterpret_cast<const uint4 *>(rhi), reinterpret_cast<const uint4 *>(rlo), rnrm, H, W, d0, d1, min_cost,
+        argmin, disp, counter, list);
+    cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
+    return SDE_OK;
+}
+
+SDE_EXPORT int64_t sde_cv_wta_split_workspace_bytes(int H, int W)
+{
+    if (H <= 0 || W <= 0) return -1;
+    return cert_ws_bytes(H, W, false);
+}
+
+SDE_EXPORT int sde_cv_wta_split(const float *fl, const float *fr, const uint16_t *fl_hi, const uint16_t *fl_lo,
+                                const float *fl_norm, const uint16_t *fr_hi, const uint16_t *fr_lo,
+                                const float *fr_norm, int H, int W, int d0, int d1, float *disp, float *min_cost,
+                                int32_t *argmin, void *workspace, int64_t workspace_bytes, void *stream)
+{
+    if (!fl || !fr || !fl_hi || !fl_lo || !fl_norm || !fr_hi || !fr_lo || !fr_norm) return SDE_ERR_ARG;
+    if (H <= 0 || W <= 0 || d0 < 0 || d1 <= d0 || (!disp && !min_cost && !argmin)) return SDE_ERR_ARG;
+    if (!workspace || workspace_bytes < cert_ws_bytes(H, W, false)) return SDE_ERR_WORKSPACE;
+    const int s = launch_cert(fl, fr, fl_hi, fl_lo, fl_norm, fr_hi, fr_lo, fr_norm, H, W, d0, d1, disp, min_cost,
+                              argmin, workspace, as_stream(stream));
+    if (s != SDE_OK) return s;
+    return launch_status();
 }
 
 SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, int d1, float *disp,
@@ -602,12 +671,19 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
     hipStream_t st = as_stream(stream);
     if (C == 64 && mode == SDE_CV_CERTIFIED) {
         if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
-        unsigned *counter = reinterpret_cast<unsigned *>(workspace);
-        int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
-        if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
-        cv_wta_fast_kernel<<<cdiv(W, FX_NX) * H, 256, 0, st>>>(fl, fr, H, W, d0, d1, min_cost, argmin, disp, counter,
-                                                               list);
-        cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
+        const int64_t npix = (int64_t)H * W;
+        char *base = reinterpret_cast<char *>(workspace) + cert_ws_bytes(H, W, false);
+        uint16_t *lhi = reinterpret_cast<uint16_t *>(base);
+        uint16_t *llo = lhi + 64 * npix;
+        uint16_t *rhi = llo + 64 * npix;
+        uint16_t *rlo = rhi + 64 * npix;
+        float *lnrm = reinterpret_cast<float *>(rlo + 64 * npix);
+        float *rnrm = lnrm + ((npix + 63) / 64) * 64;
+        feature_split_kernel<<<cdiv(npix * 16, 256), 256, 0, st>>>(fl, npix, lhi, llo, lnrm);
+        feature_split_kernel<<<cdiv(npix * 16, 256), 256, 0, st>>>(fr, npix, rhi, rlo, rnrm);
+        const int s = launch_cert(fl, fr, lhi, llo, lnrm, rhi, rlo, rnrm, H, W, d0, d1, disp, min_cost, argmin,
+                                  workspace, st);
+        if (s != SDE_OK) return s;
     } else if (C == 64) {
         dim3 grid(cdiv(W, CV_TX), H);
         cv64_kernel<SDE_SIDE_LEFT, OUT_WTA><<<grid, 256, 0, st>>>(fl, fr, H, W, d0, d1, 0, -0.0f, nullptr,

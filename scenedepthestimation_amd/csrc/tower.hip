@@ -69,13 +69,49 @@ __device__ __forceinline__ void store_tap(float2 *wt, const float4 (&r)[2])
     }
 }
 
+// Last-layer extras for the certified cost volume (see cost_volume.hip):
+// bf16 hi/lo split planes of the output features (x = hi + lo + r, RNE) and
+// an upper bound of each pixel's L2 norm.  A lane holds channels
+// mt*32 + 8g + 4h + e (e = 0..3) of its pixel in v[mt][4g + e].
+__device__ __forceinline__ void emit_split(const float (&v)[2][16], int h, size_t pix, uint16_t *ohi, uint16_t *olo)
+{
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            bf4 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float x = v[mt][4 * g + e];
+                const __bf16 hh = (__bf16)x;
+                hv[e] = hh;
+                lv[e] = (__bf16)(x - (float)hh);
+            }
+            const size_t o = pix * NF + mt * 32 + 8 * g + 4 * h;
+            *reinterpret_cast<uint2 *>(ohi + o) = __builtin_bit_cast(uint2, hv);
+            *reinterpret_cast<uint2 *>(olo + o) = __builtin_bit_cast(uint2, lv);
+        }
+}
+
+__device__ __forceinline__ void emit_norm(const float (&v)[2][16], int h, size_t pix, float *onrm)
+{
+    float ss = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; r++) ss += v[0][r] * v[0][r] + v[1][r] * v[1][r];
+    ss += __shfl_xor(ss, 32, 64);
+    if (h == 0 && pix != (size_t)-1) onrm[pix] = sqrtf(ss) * 1.000004f;   // fp32 rounding bound (64 terms)
+}
+
 // FIRST: the input tile is conv1 (Cin = 1) of the padded image, computed here.
 // LAST : no ReLU, L2-normalise over the 64 channels before the store.
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restrict__ in, int Hin, int Win,
                                                           const float *__restrict__ w1blob,
                                                           const float *__restrict__ wkblob,
-                                                          float *__restrict__ out, int Hout, int Wout)
+                                                          float *__restrict__ out, int Hout, int Wout,
+                                                          uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
+                                                          float *__restrict__ onrm)
 {
     extern __shared__ __attribute__((aligned(16))) float2 smem[];
     float2 *tile = smem;                          // TW_NPIX rows x 32 pairs
@@ -185,14 +221,17 @@ __global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restric
     }
     const int oy = ty0 + wave, ox = tx0 + j;
     if (oy < Hout && ox < Wout) {
-        float *dst = out + ((size_t)oy * Wout + ox) * NF;
+        const size_t pix = (size_t)oy * Wout + ox;
+        float *dst = out + pix * NF;
 #pragma unroll
         for (int mt = 0; mt < 2; mt++)
 #pragma unroll
             for (int g = 0; g < 4; g++)
                 *reinterpret_cast<float4 *>(dst + mt * 32 + 8 * g + 4 * h) =
                     make_float4(v[mt][4 * g], v[mt][4 * g + 1], v[mt][4 * g + 2], v[mt][4 * g + 3]);
+        if (LAST && ohi) emit_split(v, h, pix, ohi, olo);
     }
+    if (LAST && onrm) emit_norm(v, h, oy < Hout && ox < Wout ? (size_t)oy * Wout + ox : (size_t)-1, onrm);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,7 +269,9 @@ template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(512) void conv64_x6_kernel(const float *__restrict__ in, int Hin, int Win,
                                                         const float *__restrict__ w1blob,
                                                         const float *__restrict__ wkblob,
-                                                        float *__restrict__ out, int Hout, int Wout)
+                                                        float *__restrict__ out, int Hout, int Wout,
+                                                        uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
+                                                        float *__restrict__ onrm)
 {
     extern __shared__ __attribute__((aligned(16))) float4 smem4[];
     float4 *tile = smem4;                                                    // [340][16] float4
@@ -376,14 +417,17 @@ __global__ __launch_bounds__(512) void conv64_x6_kernel(const float *__restrict_
     }
     const int oy = ty0 + wave, ox = tx0 + j;
     if (oy < Hout && ox < Wout) {
-        float *dst = out + ((size_t)oy * Wout + ox) * NF;
+        const size_t pix = (size_t)oy * Wout + ox;
+        float *dst = out + pix * NF;
 #pragma unroll
         for (int mt = 0; mt < 2; mt++)
 #pragma unroll
             for (int g = 0; g < 4; g++)
                 *reinterpret_cast<float4 *>(dst + mt * 32 + 8 * g + 4 * h) =
                     make_float4(v[mt][4 * g], v[mt][4 * g + 1], v[mt][4 * g + 2], v[mt][4 * g + 3]);
+        if (LAST && ohi) emit_split(v, h, pix, ohi, olo);
     }
+    if (LAST && onrm) emit_norm(v, h, oy < Hout && ox < Wout ? (size_t)oy * Wout + ox : (size_t)-1, onrm);
 }
 
 // nlayers == 1: conv1 + L2 normalisation only (no ReLU on the last layer).
@@ -556,7 +600,7 @@ static void set_tower_attrs()
 // One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
 // layer > 2 -> one 64->64 conv on Hin x Win x 64 activations.  Output (Hin-4|Hin-2) x ... x 64.
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
-                         int flags, hipStream_t st)
+                         int flags, uint16_t *ohi, uint16_t *olo, float *onrm, hipStream_t st)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
@@ -565,7 +609,8 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
     dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
-#define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout)
+#define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, \
+                                                             (L) ? ohi : nullptr, (L) ? olo : nullptr, (L) ? onrm : nullptr)
     if (x6) {
         if (layer == 2) { if (last) SDE_CONV(conv64_x6_kernel, true, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, true, false, X6_SMEM); }
         else { if (last) SDE_CONV(conv64_x6_kernel, false, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, false, false, X6_SMEM); }
@@ -577,18 +622,23 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 }
 
 SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
-                               float *out, int flags, void *stream)
+                               float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm,
+                               void *stream)
 {
     if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
     if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
     if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
-    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, as_stream(stream));
+    if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, as_stream(stream));
     return launch_status();
 }
 
 SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
-                                 float *feat, void *workspace, int64_t workspace_bytes, int flags, void *stream)
+                                 float *feat, void *workspace, int64_t workspace_bytes, int flags, uint16_t *feat_hi,
+                                 uint16_t *feat_lo, float *feat_norm, void *stream)
 {
+    if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
+    if (nlayers == 1 && (feat_hi || feat_norm)) return SDE_ERR_ARG;
     if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
     if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
     const int64_t need = sde_tower_workspace_bytes(H, W, nlayers, nf);
@@ -606,12 +656,13 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
         buf[1] = buf[0] + h2 * w2 * NF;
     }
     int hin = Hp, win = Wp;
-    launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, st);
+    launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, feat_hi, feat_lo, feat_norm,
+                 st);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
-        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, st);
+        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, st);
         hin -= 2; win -= 2;
         cur ^= 1;
     }

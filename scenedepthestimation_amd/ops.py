@@ -115,6 +115,33 @@ def cv_wta(fl, fr, d0: int, d1: int, disp=None, min_cost=None, argmin=None, want
     return disp, min_cost, argmin
 
 
+def cv_wta_split_workspace_bytes(H: int, W: int) -> int:
+    return int(lib.sde_cv_wta_split_workspace_bytes(H, W))
+
+
+def cv_wta_split(fl, fr, split_l, split_r, d0: int, d1: int, disp=None, min_cost=None, argmin=None,
+                 workspace=None, want=("disp",)):
+    """Certified fused CV + WTA on pre-split operands (tower-emitted or feature_split)."""
+    pl, pr, H, W, C = _feat_pair(fl, fr)
+    if "disp" in want and disp is None:
+        disp = _empty((H, W), torch.float32, fl)
+    if "min" in want and min_cost is None:
+        min_cost = _empty((H, W), torch.float32, fl)
+    if "argmin" in want and argmin is None:
+        argmin = _empty((H, W), torch.int32, fl)
+    pd = _need(disp, "disp", shape=(H, W)) if disp is not None else None
+    pm = _need(min_cost, "min_cost", shape=(H, W)) if min_cost is not None else None
+    pa = _need(argmin, "argmin", dtype=torch.int32, shape=(H, W)) if argmin is not None else None
+    if workspace is None:
+        workspace = torch.empty(cv_wta_split_workspace_bytes(H, W), dtype=torch.uint8, device=fl.device)
+    lh, ll, ln = _split_ptrs(split_l, (H, W))
+    rh, rl, rn = _split_ptrs(split_r, (H, W))
+    check(lib.sde_cv_wta_split(pl, pr, lh, ll, ln, rh, rl, rn, H, W, int(d0), int(d1), pd, pm, pa,
+                               _need(workspace, "workspace", dtype=torch.uint8), workspace.numel(), _stream()),
+          "sde_cv_wta_split")
+    return disp, min_cost, argmin
+
+
 def cv_wta_fixups(workspace) -> int:
     """Number of pixels the last certified cv_wta call resolved with the exact scan (synchronises)."""
     return int(workspace[:4].view(torch.int32).item())
@@ -184,9 +211,38 @@ def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
 TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6}
 
 
-def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None, precision: str = "fp32"):
+def _split_ptrs(split, shape):
+    """split = (hi int16 [..., 64], lo int16 [..., 64], norm f32 [...]) or None -> three pointers."""
+    if split is None:
+        return None, None, None
+    hi, lo, nrm = split
+    return (_need(hi, "feat_hi", dtype=torch.int16, shape=shape + (64,)),
+            _need(lo, "feat_lo", dtype=torch.int16, shape=shape + (64,)),
+            _need(nrm, "feat_norm", shape=shape))
+
+
+def new_split(H: int, W: int, device):
+    """Buffers for bf16 split planes + norm bound of an [H,W,64] feature map."""
+    return (torch.empty((H, W, 64), dtype=torch.int16, device=device),
+            torch.empty((H, W, 64), dtype=torch.int16, device=device),
+            torch.empty((H, W), dtype=torch.float32, device=device))
+
+
+def feature_split(feat, split=None):
+    """[H,W,64] f32 -> (hi, lo, norm) for the certified cost volume (sde_feature_split)."""
+    H, W, C = feat.shape
+    if split is None:
+        split = new_split(H, W, feat.device)
+    ph, pl, pn = _split_ptrs(split, (H, W))
+    check(lib.sde_feature_split(_need(feat, "features"), H * W, C, ph, pl, pn, _stream()), "sde_feature_split")
+    return split
+
+
+def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None, precision: str = "fp32",
+                  split=None):
     """img_pad: f32 [H+2L, W+2L] -> L2-normalised features f32 [H, W, nf].
-    precision: 'fp32' (fp32 MFMA) or 'bf16x6' (exact 3-way bf16 split, 6 partial products, fp32 accumulate)."""
+    precision: 'fp32' (fp32 MFMA) or 'bf16x6' (exact 3-way bf16 split, 6 partial products, fp32 accumulate).
+    split: optional (hi, lo, norm) buffers the last layer's epilogue fills (certified cost volume input)."""
     Hp, Wp = img_pad.shape
     H, W = Hp - 2 * nlayers, Wp - 2 * nlayers
     if H <= 0 or W <= 0:
@@ -201,12 +257,13 @@ def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspa
         workspace = torch.empty(need, dtype=torch.uint8, device=img_pad.device)
     pws = _need(workspace, "workspace", dtype=torch.uint8) if need > 0 else None
     wsb = workspace.numel() if need > 0 else 0
-    check(lib.sde_tower_forward(pi, H, W, pw, nlayers, nf, po, pws, wsb, TOWER_PRECISIONS[precision], _stream()),
-          "sde_tower_forward")
+    ph, pl_, pn = _split_ptrs(split, (H, W))
+    check(lib.sde_tower_forward(pi, H, W, pw, nlayers, nf, po, pws, wsb, TOWER_PRECISIONS[precision], ph, pl_, pn,
+                                _stream()), "sde_tower_forward")
     return out
 
 
-def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32"):
+def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None):
     """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image)."""
     if layer == 2:
         Hin, Win = inp.shape
@@ -217,7 +274,7 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precis
     check(lib.sde_tower_layer(_need(inp, "layer input"), Hin, Win,
                               _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
                               nlayers, nf, layer, _need(out, "layer output", shape=oshape),
-                              TOWER_PRECISIONS[precision], _stream()),
+                              TOWER_PRECISIONS[precision], *_split_ptrs(split, oshape[:2]), _stream()),
           "sde_tower_layer")
     return out
 

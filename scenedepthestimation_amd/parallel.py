@@ -110,6 +110,7 @@ class DisparityShardedMatcher:
         full = self.full.view(self.world, 2, self.rpb, self.W, m.nf)
         for i in range(2):
             m.feat[i].copy_(full[:, i].reshape(self.world * self.rpb, self.W, m.nf)[:self.H])
+        m.split_valid = False    # assembled features: the certified call splits them itself
         return m.feat[0], m.feat[1]
 
     def match(self):

@@ -50,6 +50,10 @@ class StereoMatcher:
         self.argmin = torch.empty((H, W), dtype=torch.int32, device=dev)
         self.cv_mode = cv_mode
         self.cv_ws = torch.empty(ops.cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device=dev)
+        # bf16 split planes + norm bounds emitted by the tower's last layer (certified cost volume input)
+        self.split = [ops.new_split(H, W, dev) for _ in range(2)] if (cv_mode == "certified" and nlayers >= 2) \
+            else None
+        self.split_valid = False
         self.sgm_bufs = None
         if sgm:
             self._alloc_sgm()
@@ -66,18 +70,27 @@ class StereoMatcher:
         for i in range(2):
             ops.preprocess_u8(self.img_u8[i], self.nlayers, out=self.img_pad[i], stats=self.stats[i])
             ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
-                              precision=self.tower_precision)
+                              precision=self.tower_precision, split=self.split[i] if self.split else None)
+        self.split_valid = self.split is not None
         return self.feat[0], self.feat[1]
 
     def features_from_padded(self):
         """Tower only, on already-normalised padded images in self.img_pad."""
         for i in range(2):
             ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
-                              precision=self.tower_precision)
+                              precision=self.tower_precision, split=self.split[i] if self.split else None)
+        self.split_valid = self.split is not None
         return self.feat[0], self.feat[1]
 
     def cost_wta(self, want=("disp",)):
-        """Fused cost volume + WTA over this matcher's disparity range [d0, d1)."""
+        """Fused cost volume + WTA over this matcher's disparity range [d0, d1).  In certified mode the
+        tower-emitted split planes are used when the current features came from this matcher's tower."""
+        if self.cv_mode == "certified" and self.split_valid:
+            return ops.cv_wta_split(self.feat[0], self.feat[1], self.split[0], self.split[1], self.d0, self.d1,
+                                    disp=self.disp if "disp" in want else None,
+                                    min_cost=self.min_cost if "min" in want else None,
+                                    argmin=self.argmin if "argmin" in want else None, want=(),
+                                    workspace=self.cv_ws)
         return ops.cv_wta(self.feat[0], self.feat[1], self.d0, self.d1,
                           disp=self.disp if "disp" in want else None,
                           min_cost=self.min_cost if "min" in want else None,

@@ -72,10 +72,15 @@ def test_argument_validation_without_gpu():
     assert lib.sde_sgm_8path(1, 1, 1, 5, 8, 1, None) == ERR                                        # H < 2
     assert lib.sde_sgm_8path(1, 1, 5, 5, 513, 1, None) == ERR                                      # D > 512
     assert lib.sde_sgm_direction(1, 1, 5, 5, 8, 8, 1, None) == ERR                                 # direction
-    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, None, 0, 0, None) == ERR                    # nf != 64
-    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, None, 0, 0, None) == -3                     # workspace
-    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 4, None) == ERR                 # bad flags
-    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, 0, None) == ERR                            # layer 1
+    N = None
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, N, 0, 0, N, N, N, N) == ERR                 # nf != 64
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, N, 0, 0, N, N, N, N) == -3                  # workspace
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 4, N, N, N, N) == ERR           # bad flags
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 0, 1, N, N, N) == ERR           # hi without lo
+    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, 0, N, N, N, N) == ERR                      # layer 1
+    assert lib.sde_feature_split(1, 10, 32, 1, 1, 1, N) == ERR                                     # C != 64
+    assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace
+    assert lib.sde_cv_wta_split(1, 1, N, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 1 << 20, N) == ERR
     assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
     assert lib.sde_tower_packed_floats(0, 64) == -1
 
