@@ -203,6 +203,17 @@ int sde_sgm_penalties(const uint8_t *img, int H, int W, double P1, double P2, in
  */
 int sde_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float *S, void *stream);
 
+/*
+ * Both image sides of the reference's per-direction k loop (:1166-1203) in one
+ * launch per direction (the (cv_r, pen_r, S_r) triple may be all NULL for one
+ * side).  flags = 0: S := the 8-path sum starting from zero, so the caller need
+ * not zero S and the first direction does not read it (same values as zeroing
+ * S then accumulating); SDE_SGM_ACCUMULATE: S += path costs as sde_sgm_8path.
+ */
+#define SDE_SGM_ACCUMULATE 1
+int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r, const float *pen_r,
+                       float *S_r, int H, int W, int D, int flags, void *stream);
+
 /* One direction (0..7 in the order above) of sde_sgm_8path. */
 int sde_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int direction, float *S,
                       void *stream);

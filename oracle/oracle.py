@@ -159,14 +159,18 @@ def sgm_direction(cv_hwd, pen, direction, S=None):
     return S
 
 
-def sgm_8path(cv_hwd, pen):
-    """All 8 directions in launch order (process_functional.py:1166-1203) for one side -> S f32 [H,W,D]."""
+def sgm_8path(cv_hwd, pen, S=None):
+    """All 8 directions in launch order (process_functional.py:1166-1203) for one side -> S f32 [H,W,D].
+
+    S: optional initial S (accumulated into, in place); zeros as the reference uploads by default."""
     cv = _c32(cv_hwd)
     pen = _c32(pen)
     H, W, D = cv.shape
     if H < 2 or W < 2:
         raise ValueError("SGM needs H >= 2 and W >= 2 (the reference indexes out of bounds otherwise)")
-    S = np.zeros((H, W, D), np.float32)
+    if S is None:
+        S = np.zeros((H, W, D), np.float32)
+    assert S.dtype == np.float32 and S.shape == cv.shape and S.flags.c_contiguous
     lib().sdeo_sgm_8path(_p(cv), _p(pen), H, W, D, _p(S))
     return S
 

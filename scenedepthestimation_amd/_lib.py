@@ -26,6 +26,7 @@ SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
 SDE_TOWER_FP32, SDE_TOWER_BF16X6 = 0, 1
 SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
+SDE_SGM_ACCUMULATE = 1
 
 # name -> (restype, argtypes); must cover every function declared in include/sde.h
 SIGNATURES = {
@@ -54,6 +55,7 @@ SIGNATURES = {
     "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
                                   c_void_p]),
     "sde_sgm_8path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_sgm_8path_pair": (c_int, [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_void_p]),
     "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_lr_check": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_lrc_fill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

@@ -15,12 +15,16 @@
 // step, out-of-range neighbours (d = 0, D-1) dropped, n-1 pixels per line of n
 // (>= 2), and diagonal lines wrapping around the image with a path restart.
 //
-// Mapping: one wave64 per scanline; lane l owns DPL = ceil(D/64) consecutive
-// disparities (d = l*DPL + i) in registers, so d-1 / d+1 cross a lane boundary
-// only at i = 0 / DPL-1 (one 64-bit shuffle each) and min_d is a 6-level xor
-// butterfly.  The scanline's per-pixel loads (C and S, DPL floats per lane;
-// the two penalties, wave-uniform) are prefetched PF steps ahead in a register
-// ring so HBM latency overlaps the sequential DP.
+// Mapping: one wave64 (one workgroup) per scanline and image side, so the line,
+// the pixel sequence and the penalty addresses are wave-uniform (scalar loads).
+// Lane l owns DPL = ceil(D/64) consecutive disparities d = l*DPL + i in
+// registers: d-1 / d+1 cross a lane only at i = 0 / DPL-1 (one DPP wave_shr /
+// wave_shl per fp64 half), and min_d is a DPP butterfly (quad_perm, row_ror,
+// row_bcast) ending in one readlane -- no LDS round trips on the serial chain.
+// Each step's C and S rows (DPL floats per lane, one dwordx{DPL} load each,
+// addresses clamped so no load is predicated) are prefetched PF steps ahead in
+// a register ring, so HBM latency overlaps the sequential DP.  The left and
+// right image sides (the reference's k loop) run in the same launch (grid.y).
 #include "sde_common.h"
 
 namespace sde {
@@ -31,7 +35,7 @@ __constant__ int c_dir_dc[8] = {0, 0, +1, -1, +1, +1, -1, -1};
 __constant__ int c_dir_ch[8] = {2, 0, 6, 4, 10, 12, 8, 14};
 
 struct PathGeom {
-    int dir, dr, dc, ch, H, W, n;
+    int dr, dc, ch, H, W, n;
 };
 
 // k-th pixel of scanline `line`; restart = first pixel or diagonal wrap.
@@ -58,58 +62,142 @@ __device__ __forceinline__ void path_pixel(const PathGeom &g, int line, int k, i
     }
 }
 
+template <int N>
+struct alignas(4) FVec {
+    float v[N];
+};
+
+// DPP move of a double (two 32-bit halves); lanes outside ROW_MASK keep `v`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    int lo = (int)b, hi = (int)(b >> 32);
+    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double dmin(double a, double t) { return t < a ? t : a; }
+
+// min over the 64 lanes, returned wave-uniform
+__device__ __forceinline__ double wave_min_f64(double v)
+{
+    v = dmin(v, dpp_f64<0xB1>(v));          // quad_perm [1,0,3,2]
+    v = dmin(v, dpp_f64<0x4E>(v));          // quad_perm [2,3,0,1]
+    v = dmin(v, dpp_f64<0x124>(v));         // row_ror:4
+    v = dmin(v, dpp_f64<0x128>(v));         // row_ror:8   -> every lane holds its row's min
+    v = dmin(v, dpp_f64<0x142, 0xA>(v));    // row_bcast:15 -> rows 1, 3
+    v = dmin(v, dpp_f64<0x143, 0xC>(v));    // row_bcast:31 -> row 3 holds all four
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+struct SgmSide {
+    const float *cv;
+    const float *pen;
+    float *S;
+};
+
 template <int DPL>
 struct Slot {
-    float cst[DPL];
+    float c[DPL];
     float s[DPL];
-    double p1, p2;
+    float p1, p2;
     size_t off;     // voxel offset of (r, c, d = 0)
     bool restart;
 };
 
-template <int DPL>
-__device__ __forceinline__ void issue(const PathGeom &g, int line, int k, const float *__restrict__ cv,
-                                      const float *__restrict__ pen, const float *__restrict__ S, int D,
-                                      int dbase, Slot<DPL> &sl)
-{
+// Incremental walk along a scanline (wave-uniform scalars; no divisions).  Same
+// pixel sequence as path_pixel: diagonal lines wrap around the image with a
+// path restart.  Steps past the end of the line are clamped into the image (the
+// kernel re-reads valid memory there and stores nothing).
+struct Walker {
     int r, c;
     bool restart;
-    path_pixel(g, line, k, r, c, restart);
-    sl.restart = restart;
-    sl.off = ((size_t)r * g.W + c) * D;
-    const int pr = r - g.dr, pc = c - g.dc;
-    double p1 = 0.0;
-    if (!restart && pr >= 0 && pr < g.H && pc >= 0 && pc < g.W) p1 = (double)pen[((size_t)pr * g.W + pc) * 16 + g.ch];
-    sl.p1 = p1;
-    sl.p2 = (double)pen[((size_t)r * g.W + c) * 16 + g.ch + 1];
+    __device__ __forceinline__ void init(const PathGeom &g, int line)
+    {
+        if (g.dc == 0) { c = line; r = g.dr > 0 ? 0 : g.H - 1; }
+        else if (g.dr == 0) { r = line; c = g.dc > 0 ? 0 : g.W - 1; }
+        else { r = g.dr > 0 ? 0 : g.H - 1; c = line; }
+        restart = true;
+    }
+    __device__ __forceinline__ void advance(const PathGeom &g)
+    {
+        r += g.dr;
+        c += g.dc;
+        restart = false;
+        if (g.dr != 0 && g.dc != 0) {
+            if (c >= g.W) { c = 0; restart = true; }
+            else if (c < 0) { c = g.W - 1; restart = true; }
+        }
+    }
+};
+
+// VEC: D % DPL == 0, every lane's DPL disparities are all valid or all invalid
+// and move as one dwordx{DPL}; otherwise per-element loads with clamped d.
+template <int DPL, bool VEC, bool FIRST>
+__device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const SgmSide &sd, int D, int dbase,
+                                      Slot<DPL> &sl)
+{
+    const int r = min(max(w.r, 0), g.H - 1), c = min(max(w.c, 0), g.W - 1);
+    const size_t px = (size_t)r * g.W + c;
+    int pr = r - g.dr, pc = c - g.dc;
+    const bool pin = pr >= 0 && pr < g.H && pc >= 0 && pc < g.W;
+    pr = pin ? pr : r;
+    pc = pin ? pc : c;
+    const float p1 = sd.pen[((size_t)pr * g.W + pc) * 16 + g.ch];
+    sl.p1 = pin ? p1 : 0.0f;
+    sl.p2 = sd.pen[px * 16 + g.ch + 1];
+    sl.restart = w.restart;
+    const size_t off = px * D;
+    sl.off = off;
+    if (VEC) {
+        const size_t o = off + (dbase < D ? dbase : 0);
+        const FVec<DPL> cv = *reinterpret_cast<const FVec<DPL> *>(sd.cv + o);
 #pragma unroll
-    for (int i = 0; i < DPL; i++) {
-        const int d = dbase + i;
-        sl.cst[i] = d < D ? cv[sl.off + d] : 0.0f;
-        sl.s[i] = d < D ? S[sl.off + d] : 0.0f;
+        for (int i = 0; i < DPL; i++) sl.c[i] = cv.v[i];
+        if (!FIRST) {
+            const FVec<DPL> sv = *reinterpret_cast<const FVec<DPL> *>(sd.S + o);
+#pragma unroll
+            for (int i = 0; i < DPL; i++) sl.s[i] = sv.v[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < DPL; i++) {
+            const int d = dbase + i < D ? dbase + i : D - 1;
+            sl.c[i] = sd.cv[off + d];
+            if (!FIRST) sl.s[i] = sd.S[off + d];
+        }
     }
 }
 
-template <int DPL, int PF>
-__global__ __launch_bounds__(256) void sgm_dir_kernel(const float *__restrict__ cv, const float *__restrict__ pen,
-                                                      int H, int W, int D, int dir, float *__restrict__ S)
+template <int DPL, int PF, bool VEC, bool FIRST>
+__global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
+    const SgmSide sd = blockIdx.y ? s1 : s0;
     PathGeom g;
-    g.dir = dir; g.dr = c_dir_dr[dir]; g.dc = c_dir_dc[dir]; g.ch = c_dir_ch[dir];
+    g.dr = c_dir_dr[dir]; g.dc = c_dir_dc[dir]; g.ch = c_dir_ch[dir];
     g.H = H; g.W = W;
     const int nlen = (g.dc != 0 && g.dr == 0) ? W : H;
     g.n = nlen - 1 > 2 ? nlen - 1 : 2;
-    const int nlines = (g.dc != 0 && g.dr == 0) ? H : W;
-    const int lane = threadIdx.x & 63;
-    const int line = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (line >= nlines) return;            // whole wave leaves together
+    const int line = blockIdx.x;
+    const int lane = threadIdx.x;
     const int dbase = lane * DPL;
     const double INF = __builtin_inf();
 
+    // Every load is unconditional (steps past the end re-read a clamped pixel):
+    // a predicated load would make the ring slot a phi and force an early wait.
     Slot<DPL> ring[PF];
+    Walker ahead;
+    ahead.init(g, line);
 #pragma unroll
-    for (int j = 0; j < PF; j++)
-        if (j < g.n) issue<DPL>(g, line, j, cv, pen, S, D, dbase, ring[j]);
+    for (int j = 0; j < PF; j++) {
+        issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
+        ahead.advance(g);
+    }
 
     double L[DPL];
     double m = 1.0, mP2 = 1.0;
@@ -119,76 +207,106 @@ __global__ __launch_bounds__(256) void sgm_dir_kernel(const float *__restrict__ 
     for (int k0 = 0; k0 < g.n; k0 += PF) {
 #pragma unroll
         for (int j = 0; j < PF; j++) {
-            const int k = k0 + j;
-            if (k >= g.n) break;
-            Slot<DPL> &sl = ring[j];
+            const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
+            const Slot<DPL> &sl = ring[j];
             double Ln[DPL];
             if (sl.restart) {
 #pragma unroll
-                for (int i = 0; i < DPL; i++) Ln[i] = (double)sl.cst[i];
+                for (int i = 0; i < DPL; i++) Ln[i] = (double)sl.c[i];
             } else {
-                const double lo = __shfl_up(L[DPL - 1], 1, 64);     // L'(dbase - 1)
-                const double hi = __shfl_down(L[0], 1, 64);         // L'(dbase + DPL)
+                const double p1 = (double)sl.p1;
+                const double lo = dpp_f64<0x138>(L[DPL - 1]);   // wave_shr:1 -> L'(dbase - 1)
+                const double hi = dpp_f64<0x130>(L[0]);         // wave_shl:1 -> L'(dbase + DPL)
 #pragma unroll
                 for (int i = 0; i < DPL; i++) {
                     const int d = dbase + i;
                     double b = L[i];
                     const double left = i > 0 ? L[i - 1] : lo;
                     const double right = i < DPL - 1 ? L[i + 1] : hi;
-                    if (d > 0) { const double t = left + sl.p1; b = t < b ? t : b; }
-                    if (d < D - 1) { const double t = right + sl.p1; b = t < b ? t : b; }
+                    if (d > 0) { const double t = left + p1; b = t < b ? t : b; }
+                    if (d < D - 1) { const double t = right + p1; b = t < b ? t : b; }
                     b = mP2 < b ? mP2 : b;
-                    Ln[i] = (double)sl.cst[i] + (b - m);
+                    Ln[i] = (double)sl.c[i] + (b - m);
                 }
             }
+            float o[DPL];
 #pragma unroll
-            for (int i = 0; i < DPL; i++) {
-                const int d = dbase + i;
-                if (d < D) S[sl.off + d] = (float)((double)sl.s[i] + Ln[i]);
-            }
-            if (k < g.n - 1) {
-                double mm = INF;
+            for (int i = 0; i < DPL; i++)
+                o[i] = FIRST ? (float)(0.0 + Ln[i]) : (float)((double)sl.s[i] + Ln[i]);
+            if (k < g.n) {
+                if (VEC) {
+                    if (dbase < D) {
+                        FVec<DPL> ov;
 #pragma unroll
-                for (int i = 0; i < DPL; i++)
-                    if (dbase + i < D) mm = Ln[i] < mm ? Ln[i] : mm;
+                        for (int i = 0; i < DPL; i++) ov.v[i] = o[i];
+                        *reinterpret_cast<FVec<DPL> *>(sd.S + sl.off + dbase) = ov;
+                    }
+                } else {
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const double t = __shfl_xor(mm, o, 64);
-                    mm = t < mm ? t : mm;
+                    for (int i = 0; i < DPL; i++)
+                        if (dbase + i < D) sd.S[sl.off + dbase + i] = o[i];
                 }
-                m = mm;
-                mP2 = mm + sl.p2;
             }
-            const double p2_unused = sl.p2;
-            (void)p2_unused;
+            double mm = INF;
+#pragma unroll
+            for (int i = 0; i < DPL; i++)
+                if (dbase + i < D) mm = Ln[i] < mm ? Ln[i] : mm;
+            m = wave_min_f64(mm);
+            mP2 = m + (double)sl.p2;
 #pragma unroll
             for (int i = 0; i < DPL; i++) L[i] = Ln[i];
-            if (k + PF < g.n) issue<DPL>(g, line, k + PF, cv, pen, S, D, dbase, ring[j]);
+            issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
+            ahead.advance(g);
+        }
+    }
+    if (FIRST) {
+        // S := 0 + paths: pixels this direction never visits (UD stops at row n-1) start at 0
+        for (int r = g.n; r < H; r++) {
+            const size_t off = ((size_t)r * W + line) * D;
+#pragma unroll
+            for (int i = 0; i < DPL; i++)
+                if (dbase + i < D) sd.S[off + dbase + i] = 0.0f;
         }
     }
 }
 
-template <int DPL>
-static void launch_dir(const float *cv, const float *pen, int H, int W, int D, int dir, float *S, hipStream_t st)
+template <int DPL, bool VEC, bool FIRST>
+static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
+                        hipStream_t st)
 {
     const bool horiz = (dir == 2 || dir == 3);
     const int nlines = horiz ? H : W;
-    sgm_dir_kernel<DPL, 8><<<cdiv(nlines, 4), 256, 0, st>>>(cv, pen, H, W, D, dir, S);
+    constexpr int PF = DPL <= 4 ? 8 : 4;
+    sgm_scan_kernel<DPL, PF, VEC, FIRST><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
 }
 
-static int sgm_direction_impl(const float *cv, const float *pen, int H, int W, int D, int dir, float *S,
-                              hipStream_t st)
+template <int DPL>
+static void launch_dpl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, bool first,
+                       hipStream_t st)
 {
-    const int dpl = (D + 63) / 64;
-    switch (dpl) {
-    case 1: launch_dir<1>(cv, pen, H, W, D, dir, S, st); break;
-    case 2: launch_dir<2>(cv, pen, H, W, D, dir, S, st); break;
-    case 3: launch_dir<3>(cv, pen, H, W, D, dir, S, st); break;
-    case 4: launch_dir<4>(cv, pen, H, W, D, dir, S, st); break;
-    case 5: launch_dir<5>(cv, pen, H, W, D, dir, S, st); break;
-    case 6: launch_dir<6>(cv, pen, H, W, D, dir, S, st); break;
-    case 7: launch_dir<7>(cv, pen, H, W, D, dir, S, st); break;
-    case 8: launch_dir<8>(cv, pen, H, W, D, dir, S, st); break;
+    const bool vec = (D % DPL) == 0;
+    if (vec) {
+        if (first) launch_scan<DPL, true, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, true, false>(a, b, nsides, H, W, D, dir, st);
+    } else {
+        if (first) launch_scan<DPL, false, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, false, false>(a, b, nsides, H, W, D, dir, st);
+    }
+}
+
+// One direction over one or two sides; first: S := f32(0 + L) (no S read).
+static int sgm_direction_impl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
+                              bool first, hipStream_t st)
+{
+    switch ((D + 63) / 64) {
+    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, first, st); break;
     default: return SDE_ERR_ARG;
     }
     return SDE_OK;
@@ -316,16 +434,29 @@ SDE_EXPORT int sde_sgm_direction(const float *cv, const float *pen, int H, int W
 {
     if (!cv || !pen || !S || H < 2 || W < 2 || D <= 0 || D > 512 || direction < 0 || direction > 7)
         return SDE_ERR_ARG;
-    const int s = sgm_direction_impl(cv, pen, H, W, D, direction, S, as_stream(stream));
+    const SgmSide a{cv, pen, S};
+    const int s = sgm_direction_impl(a, a, 1, H, W, D, direction, false, as_stream(stream));
     if (s != SDE_OK) return s;
     return launch_status();
 }
 
 SDE_EXPORT int sde_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float *S, void *stream)
 {
-    if (!cv || !pen || !S || H < 2 || W < 2 || D <= 0 || D > 512) return SDE_ERR_ARG;
+    return sde_sgm_8path_pair(cv, pen, S, nullptr, nullptr, nullptr, H, W, D, SDE_SGM_ACCUMULATE, stream);
+}
+
+SDE_EXPORT int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r,
+                                  const float *pen_r, float *S_r, int H, int W, int D, int flags, void *stream)
+{
+    if (!cv_l || !pen_l || !S_l || H < 2 || W < 2 || D <= 0 || D > 512 || (flags & ~SDE_SGM_ACCUMULATE))
+        return SDE_ERR_ARG;
+    const bool two = cv_r || pen_r || S_r;
+    if (two && (!cv_r || !pen_r || !S_r)) return SDE_ERR_ARG;
+    const SgmSide a{cv_l, pen_l, S_l};
+    const SgmSide b = two ? SgmSide{cv_r, pen_r, S_r} : a;
     for (int dir = 0; dir < 8; dir++) {
-        const int s = sgm_direction_impl(cv, pen, H, W, D, dir, S, as_stream(stream));
+        const bool first = dir == 0 && !(flags & SDE_SGM_ACCUMULATE);   // UD: line = column
+        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, as_stream(stream));
         if (s != SDE_OK) return s;
     }
     return launch_status();

@@ -316,8 +316,25 @@ def sgm_8path(cv_hwd, pen, S=None):
     pp = _need(pen, "penalties", shape=(H, W, 16))
     if S is None:
         S = torch.zeros((H, W, D), dtype=torch.float32, device=cv_hwd.device)
+    # accumulates into S (the caller zeroes it, as the reference uploads np.zeros)
     check(lib.sde_sgm_8path(pc, pp, H, W, D, _need(S, "S", shape=(H, W, D)), _stream()), "sde_sgm_8path")
     return S
+
+
+def sgm_8path_pair(cv_l, pen_l, S_l, cv_r=None, pen_r=None, S_r=None, accumulate=False):
+    """8-path SGM of both image sides, one launch per direction (sde_sgm_8path_pair).
+
+    accumulate=False: S := the 8-path sum from zero (S need not be zeroed)."""
+    H, W, D = cv_l.shape
+    args = [_need(cv_l, "cost volume"), _need(pen_l, "penalties", shape=(H, W, 16)), _need(S_l, "S", shape=(H, W, D))]
+    if cv_r is None:
+        args += [None, None, None]
+    else:
+        args += [_need(cv_r, "cost volume", shape=(H, W, D)), _need(pen_r, "penalties", shape=(H, W, 16)),
+                 _need(S_r, "S", shape=(H, W, D))]
+    check(lib.sde_sgm_8path_pair(*args, H, W, D, _lib.SDE_SGM_ACCUMULATE if accumulate else 0, _stream()),
+          "sde_sgm_8path_pair")
+    return S_l, S_r
 
 
 def sgm_direction(cv_hwd, pen, direction: int, S):

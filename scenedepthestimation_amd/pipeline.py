@@ -142,9 +142,8 @@ class StereoMatcher:
         t = mark("cost_volume", t)
         ops.sgm_penalties(img_l, out=b["pen"][0])
         ops.sgm_penalties(img_r, out=b["pen"][1])
-        for k in range(2):
-            b["S"][k].zero_()
-            ops.sgm_8path(b["cv"][k], b["pen"][k], S=b["S"][k])
+        # both sides per launch (the reference's k loop); S := 8-path sum, no zero-fill pass
+        ops.sgm_8path_pair(b["cv"][0], b["pen"][0], b["S"][0], b["cv"][1], b["pen"][1], b["S"][1])
         t = mark("sgm", t)
         for k in range(2):
             ops.wta(b["S"][k], layout="HWD", rule="d0", out=b["disp"][k])

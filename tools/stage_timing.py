@@ -47,6 +47,11 @@ def main(H=1024, W=1024, D=192):
         out[f"sgm_dir{d}_ms"] = timeit(lambda: ops.sgm_direction(cvl, pen, d, S), reps=2)
     out["sgm_8path_ms"] = timeit(lambda: ops.sgm_8path(cvl, pen, S=S), reps=2)
     out["sgm_GBs_algorithmic"] = 96.0 * vox / (out["sgm_8path_ms"] * 1e-3) / 1e9
+    penr = ops.sgm_penalties(il)
+    S2 = torch.empty((H, W, D), device="cuda")
+    out["sgm_8path_pair_ms"] = timeit(lambda: ops.sgm_8path_pair(cvl, pen, S, cvr, penr, S2), reps=2)
+    # overwrite mode: first direction reads C and writes S (8 B), the other 7 read C, S and write S (12 B)
+    out["sgm_pair_GBs_algorithmic"] = 2 * 92.0 * vox / (out["sgm_8path_pair_ms"] * 1e-3) / 1e9
     out["cv_dhw_GBs_algorithmic"] = 4.0 * H * W * (2 * 64 + D) / (out["cv_dhw_ms"] * 1e-3) / 1e9
     print(json.dumps(out), flush=True)
 
