@@ -218,6 +218,33 @@ int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const 
 int sde_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int direction, float *S,
                       void *stream);
 
+/* ---------------------------------------------------------------------- */
+/* Cross-based cost aggregation.  BUILD-DEFINED: the reference has none      */
+/* (SURVEY.md sec. 0.3 -- only the buffer name d_cost_volumel_after_aggr,   */
+/* process_functional.py:268,347, and an unused timer label, match.py:98);  */
+/* the definition is restated on the CPU under oracle/ (parity unpinned vs */
+/* the reference, bit-exact vs that restatement).                          */
+/* ---------------------------------------------------------------------- */
+#define SDE_CBCA_MAX_L1 32
+
+/*
+ * Cross arms of an f32 image (row pitch in elements, e.g. the z-normalised
+ * interior of the tower's padded input): for left/right/up/down the largest
+ * k <= L1-1 with |I(p) - I(p + j*dir)| < tau for all 1 <= j <= k inside the
+ * image.  arms u32 [H][W] = l | r<<8 | u<<16 | d<<24.
+ */
+int sde_cbca_arms(const float *img, int64_t pitch, int H, int W, int L1, float tau, uint32_t *arms, void *stream);
+
+/*
+ * iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv) on an
+ * [H][W][D] volume, in place in cv (tmp: same size, scratch).  side
+ * SDE_SIDE_LEFT: left-referenced volume, the other pixel is x - d (arms_ref =
+ * left image arms, arms_other = right); SDE_SIDE_RIGHT: x + d.  L1 as given to
+ * sde_cbca_arms (arms must not exceed L1 - 1).
+ */
+int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W, int D,
+             int side, int L1, int iters, void *stream);
+
 /* is_error_match_kernel (process_functional.py:977-1000): lrc_l/lrc_r u8 [H][W], caller-zeroed. */
 int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,
                  void *stream);

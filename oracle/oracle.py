@@ -52,6 +52,10 @@ def lib():
         L.sdeo_median5.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.sdeo_tower_forward.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(_f32p), ctypes.POINTER(_f32p), _f32p]
+        _u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.sdeo_cbca_arms.argtypes = [_f32p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                     _u32p]
+        L.sdeo_cbca.argtypes = [_f32p, _f32p, _u32p, _u32p] + [ctypes.c_int] * 5
         _lib = L
     return _lib
 
@@ -238,3 +242,29 @@ def pad_image(image, patch=11):
     s = (patch - 1) // 2
     out[s:s + H, s:s + W] = x
     return out
+
+
+# --------------------------------------------------------------------------
+# Cross-based cost aggregation: BUILD-DEFINED (absent in the reference,
+# SURVEY.md sec. 0.3) -- parity unpinned; definition in sde_oracle.c.
+# --------------------------------------------------------------------------
+def cbca_arms(img, L1=14, tau=0.02):
+    """Cross arms of an f32 [H,W] image -> u32 [H,W] packed left | right<<8 | up<<16 | down<<24."""
+    im = _c32(img)
+    H, W = im.shape
+    out = np.empty((H, W), np.uint32)
+    lib().sdeo_cbca_arms(_p(im), W, H, W, int(L1), float(tau), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    return out
+
+
+def cbca(cv_hwd, arms_ref, arms_other, side="left", iters=1):
+    """iters x (horizontal then vertical cross-support mean) of an [H,W,D] volume (new array)."""
+    cv = np.array(cv_hwd, dtype=np.float32, order="C", copy=True)
+    H, W, D = cv.shape
+    tmp = np.empty_like(cv)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    a = np.ascontiguousarray(arms_ref, dtype=np.uint32)
+    b = np.ascontiguousarray(arms_other, dtype=np.uint32)
+    lib().sdeo_cbca(_p(cv), _p(tmp), a.ctypes.data_as(u32p), b.ctypes.data_as(u32p), H, W, D,
+                    1 if side == "left" else 2, int(iters))
+    return cv

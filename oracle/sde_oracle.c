@@ -450,3 +450,100 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
     }
     free(cur);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Cross-based cost aggregation -- BUILD-DEFINED, PARITY UNPINNED.           */
+/* The reference has none (only the buffer name          */
+/* d_cost_volumel_after_aggr, process_functional.py:268,347, and an unused   */
+/* timer label, match.py:98).  Definition (MC-CNN-style cross support):      */
+/*  arms: for pixel p and direction left/right/up/down, the largest k in     */
+/*   [0, L1-1] such that every q = p + j*dir, 1 <= j <= k, is inside the     */
+/*   image and fabsf(I(p) - I(q)) < tau (fp32).  Packed l | r<<8 | u<<16 |   */
+/*   d<<24.                                                                  */
+/*  voxel support (p, d): the other image's pixel is o = x - d (left-        */
+/*   referenced volume) or x + d (right-referenced); if o is outside the     */
+/*   image the support is {p}; else every arm is min(ref arm at p, other     */
+/*   arm at o).                                                              */
+/*  one iteration: horizontal pass T(p,d) = sum_{j=-hl..hr} C(y,x+j,d), then */
+/*   vertical pass C'(p,d) = (sum_{i=-vu..vd} T(y+i,x,d)) / cnt with cnt =   */
+/*   sum_i (hl+hr+1)(y+i, x, d): the mean over the union of the horizontal   */
+/*   segments hanging off p's vertical segment.  Sums are fp32, sequential   */
+/*   in ascending offset from 0.0f; cnt is exact; one IEEE fp32 division.    */
+/* ------------------------------------------------------------------------ */
+EXPORT void sdeo_cbca_arms(const float *img, long pitch, int H, int W, int L1, float tau, uint32_t *arms)
+{
+    static const int dys[4] = {0, 0, -1, 1}, dxs[4] = {-1, 1, 0, 0};
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            const float c = img[(size_t)y * pitch + x];
+            uint32_t packed = 0;
+            for (int k = 0; k < 4; k++) {
+                int len = 0;
+                while (len + 1 <= L1 - 1) {
+                    const int yy = y + (len + 1) * dys[k], xx = x + (len + 1) * dxs[k];
+                    if (yy < 0 || yy >= H || xx < 0 || xx >= W) break;
+                    if (!(fabsf(c - img[(size_t)yy * pitch + xx]) < tau)) break;
+                    len++;
+                }
+                packed |= (uint32_t)len << (8 * k);
+            }
+            arms[(size_t)y * W + x] = packed;
+        }
+}
+
+static inline void cbca_support(const uint32_t *ref, const uint32_t *oth, int W, int y, int x, int d, int side,
+                                int *a)
+{
+    const int o = side == 1 ? x - d : x + d;
+    if (o < 0 || o >= W) { a[0] = a[1] = a[2] = a[3] = 0; return; }
+    const uint32_t p = ref[(size_t)y * W + x], q = oth[(size_t)y * W + o];
+    for (int k = 0; k < 4; k++) {
+        const int u = (p >> (8 * k)) & 255, v = (q >> (8 * k)) & 255;
+        a[k] = u < v ? u : v;
+    }
+}
+
+/* side: 1 = left-referenced volume (other pixel x - d), 2 = right-referenced (x + d). */
+EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
+                            int D, int side)
+{
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D; d++) {
+                int a[4];
+                cbca_support(ref, oth, W, y, x, d, side, a);
+                float acc = 0.0f;
+                for (int j = -a[0]; j <= a[1]; j++) acc += src[((size_t)y * W + x + j) * D + d];
+                dst[((size_t)y * W + x) * D + d] = acc;
+            }
+}
+
+EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
+                            int D, int side)
+{
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D; d++) {
+                int a[4];
+                cbca_support(ref, oth, W, y, x, d, side, a);
+                float acc = 0.0f;
+                int cnt = 0;
+                for (int i = -a[2]; i <= a[3]; i++) {
+                    int b[4];
+                    cbca_support(ref, oth, W, y + i, x, d, side, b);
+                    acc += src[((size_t)(y + i) * W + x) * D + d];
+                    cnt += b[0] + b[1] + 1;
+                }
+                dst[((size_t)y * W + x) * D + d] = acc / (float)cnt;
+            }
+}
+
+/* iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv); result in cv. */
+EXPORT void sdeo_cbca(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D, int side,
+                      int iters)
+{
+    for (int it = 0; it < iters; it++) {
+        sdeo_cbca_hpass(cv, tmp, ref, oth, H, W, D, side);
+        sdeo_cbca_vpass(tmp, cv, ref, oth, H, W, D, side);
+    }
+}

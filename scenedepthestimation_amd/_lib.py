@@ -57,6 +57,8 @@ SIGNATURES = {
     "sde_sgm_8path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_sgm_8path_pair": (c_int, [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_void_p]),
     "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "sde_cbca_arms": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]),
+    "sde_cbca": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p]),
     "sde_lr_check": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_lrc_fill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sde_median5": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),

@@ -344,6 +344,40 @@ def sgm_direction(cv_hwd, pen, direction: int, S):
     return S
 
 
+# ----------------------------------------------------------------------------
+# Cross-based cost aggregation (build-defined; the reference has none)
+# ----------------------------------------------------------------------------
+CBCA_MAX_L1 = 32
+
+
+def cbca_arms(img, L1=14, tau=0.02, out=None):
+    """Cross arms of an f32 [H,W] device image (row-strided views allowed, e.g. the interior of the tower's
+    padded input) -> int32-viewed u32 [H,W] packed l | r<<8 | u<<16 | d<<24 (sde_cbca_arms)."""
+    if not isinstance(img, torch.Tensor) or img.dim() != 2 or img.dtype != torch.float32 or not img.is_cuda:
+        raise ValueError("image must be a 2-D float32 GPU tensor")
+    if img.stride(1) != 1:
+        raise ValueError("image rows must be contiguous")
+    H, W = img.shape
+    if out is None:
+        out = _empty((H, W), torch.int32, img)
+    check(lib.sde_cbca_arms(img.data_ptr(), img.stride(0), H, W, int(L1), float(tau),
+                            _need(out, "arms", dtype=torch.int32, shape=(H, W)), _stream()), "sde_cbca_arms")
+    return out
+
+
+def cbca(cv_hwd, arms_ref, arms_other, side="left", L1=14, iters=2, tmp=None):
+    """In-place cross-based aggregation of an [H,W,D] volume (sde_cbca); tmp: same-size scratch."""
+    H, W, D = cv_hwd.shape
+    if tmp is None:
+        tmp = torch.empty_like(cv_hwd)
+    sd = {"left": SDE_SIDE_LEFT, "right": SDE_SIDE_RIGHT}[side]
+    check(lib.sde_cbca(_need(cv_hwd, "cost volume"), _need(tmp, "tmp", shape=(H, W, D)),
+                       _need(arms_ref, "arms_ref", dtype=torch.int32, shape=(H, W)),
+                       _need(arms_other, "arms_other", dtype=torch.int32, shape=(H, W)), H, W, D, sd, int(L1),
+                       int(iters), _stream()), "sde_cbca")
+    return cv_hwd
+
+
 def lr_check(disp_l, disp_r, lrc_l=None, lrc_r=None):
     H, W = disp_l.shape
     if lrc_l is None:

@@ -25,8 +25,10 @@ from . import mc_cnn, ops
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
                  nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6",
-                 cv_mode: str = "certified"):
+                 cv_mode: str = "certified", cbca_iters: int = 0, cbca_L1: int = 14, cbca_tau: float = 0.02):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)
+        # cross-based aggregation before SGM (build-defined stage; 0 = the reference's GPU path)
+        self.cbca_iters, self.cbca_L1, self.cbca_tau = int(cbca_iters), int(cbca_L1), float(cbca_tau)
         self.nlayers, self.nf = int(nlayers), int(nf)
         if tower_precision not in ops.TOWER_PRECISIONS:
             raise ValueError(f"tower_precision must be one of {sorted(ops.TOWER_PRECISIONS)}")
@@ -114,6 +116,24 @@ class StereoMatcher:
             lrc=[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)],
             disp_a=torch.empty((H, W), dtype=torch.float32, device=dev),
         )
+        if self.cbca_iters > 0:
+            self.sgm_bufs["arms"] = [torch.empty((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
+            self.sgm_bufs["cbca_tmp"] = torch.empty((H, W, D), dtype=torch.float32, device=dev)
+
+    def cbca(self, cv_l, cv_r, img_l, img_r):
+        """Cross-based aggregation of the L/R [H,W,D] volumes in place (build-defined).
+        Arms come from the z-normalised images (the tower's input normalisation)."""
+        if self.sgm_bufs is None or "arms" not in self.sgm_bufs:
+            saved, self.cbca_iters = self.cbca_iters, max(self.cbca_iters, 1)
+            self._alloc_sgm()
+            self.cbca_iters = saved
+        b, P, H, W = self.sgm_bufs, self.nlayers, self.H, self.W
+        for k, img in enumerate((img_l, img_r)):
+            ops.preprocess_u8(img, P, out=self.img_pad[k], stats=self.stats[k])
+            ops.cbca_arms(self.img_pad[k][P:P + H, P:P + W], self.cbca_L1, self.cbca_tau, out=b["arms"][k])
+        ops.cbca(cv_l, b["arms"][0], b["arms"][1], "left", self.cbca_L1, self.cbca_iters, tmp=b["cbca_tmp"])
+        ops.cbca(cv_r, b["arms"][1], b["arms"][0], "right", self.cbca_L1, self.cbca_iters, tmp=b["cbca_tmp"])
+        return cv_l, cv_r
 
     def sgm_path(self, fl=None, fr=None, img_l=None, img_r=None, timings=None, post=True):
         """process_functional.py:1093-1267 on device tensors; returns (disp_l, disp_r).
@@ -140,6 +160,9 @@ class StereoMatcher:
         ops.cost_volume(fl, fr, self.D, layout="HWD", right=True, invalid=1.0,
                         out_left=b["cv"][0], out_right=b["cv"][1])
         t = mark("cost_volume", t)
+        if self.cbca_iters > 0:
+            self.cbca(b["cv"][0], b["cv"][1], img_l, img_r)
+            t = mark("cbca", t)
         ops.sgm_penalties(img_l, out=b["pen"][0])
         ops.sgm_penalties(img_r, out=b["pen"][1])
         # both sides per launch (the reference's k loop); S := 8-path sum, no zero-fill pass

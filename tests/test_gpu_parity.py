@@ -225,6 +225,64 @@ def test_sgm_8path_pair_bit_exact(gpu, oracle, H, W, D):
     assert host(got).tobytes() == want.tobytes()
 
 
+# ----------------------------------------------------------------------------
+# Cross-based aggregation (build-defined: bit-exact vs the oracle's restatement, parity unpinned vs the reference)
+# ----------------------------------------------------------------------------
+def _cbca_images(rng, H, W):
+    base = rng.integers(0, 4, (H, W)).astype(np.float32) * 0.05
+    return (np.repeat(base[:, ::3], 3, axis=1)[:, :W] + rng.standard_normal((H, W)).astype(np.float32) * 0.003)
+
+
+@pytest.mark.parametrize("L1,tau", [(14, 0.02), (32, 0.08), (1, 1.0)])
+def test_cbca_arms_bit_exact(gpu, oracle, L1, tau):
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(L1)
+    img = _cbca_images(rng, 37, 70)
+    pad = np.zeros((37 + 10, 70 + 10), np.float32)
+    pad[5:-5, 5:-5] = img
+    d = dev(pad)
+    got = host(ops.cbca_arms(d[5:-5, 5:-5], L1, tau)).view(np.uint32)    # row-strided interior view
+    assert np.array_equal(got, oracle.cbca_arms(img, L1, tau))
+
+
+@pytest.mark.parametrize("H,W,D,L1,iters,side", [(23, 61, 40, 14, 2, "left"), (40, 33, 100, 16, 1, "right"),
+                                                 (9, 130, 64, 20, 1, "left"), (70, 12, 7, 32, 2, "right"),
+                                                 (5, 5, 3, 14, 0, "left")])
+def test_cbca_bit_exact(gpu, oracle, H, W, D, L1, iters, side):
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(H * W + D)
+    il, ir = _cbca_images(rng, H, W), _cbca_images(rng, H, W)
+    al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
+    ref, oth = (al, ar) if side == "left" else (ar, al)
+    cv = rng.standard_normal((H, W, D)).astype(np.float32)
+    want = oracle.cbca(cv, ref, oth, side, iters)
+    got = dev(cv)
+    ops.cbca(got, dev(ref.view(np.int32)), dev(oth.view(np.int32)), side, L1, iters)
+    assert host(got).tobytes() == want.tobytes()
+
+
+def test_matcher_cbca_sgm_end_to_end(gpu, oracle):
+    """StereoMatcher.sgm_path with CBCA before SGM == the oracle composition on the same inputs."""
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import features, stereo_pair
+    H, W, D = 24, 50, 16
+    left, right, _ = stereo_pair(H, W, D, seed=4)
+    fl, fr = features(H, W, seed=5), features(H, W, seed=6)
+    m = StereoMatcher(H, W, D, weights="synthetic", cbca_iters=2, cbca_L1=14, cbca_tau=0.5)
+    dl, dr = m.sgm_path(fl=dev(fl), fr=dev(fr), img_l=dev(left), img_r=dev(right), post=False)
+    P = m.nlayers
+    zl = host(m.img_pad[0])[P:P + H, P:P + W]      # the device z-norm the arms were built from
+    zr = host(m.img_pad[1])[P:P + H, P:P + W]
+    al, ar = oracle.cbca_arms(zl, 14, 0.5), oracle.cbca_arms(zr, 14, 0.5)
+    assert ((al & 255) > 0).mean() > 0.2              # the arms are not trivial at this tau
+    cl, cr = oracle.cost_volume_hwd(fl, fr, D, invalid=1.0, right=True)
+    cl, cr = oracle.cbca(cl, al, ar, "left", 2), oracle.cbca(cr, ar, al, "right", 2)
+    Sl = oracle.sgm_8path(cl, oracle.sgm_penalties(left))
+    Sr = oracle.sgm_8path(cr, oracle.sgm_penalties(right))
+    assert np.array_equal(host(dl), oracle.wta_sgm(Sl))
+    assert np.array_equal(host(dr), oracle.wta_sgm(Sr))
+
+
 def test_post_processing_bit_exact(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(12)

@@ -53,6 +53,14 @@ def main(H=1024, W=1024, D=192):
     # overwrite mode: first direction reads C and writes S (8 B), the other 7 read C, S and write S (12 B)
     out["sgm_pair_GBs_algorithmic"] = 2 * 92.0 * vox / (out["sgm_8path_pair_ms"] * 1e-3) / 1e9
     out["cv_dhw_GBs_algorithmic"] = 4.0 * H * W * (2 * 64 + D) / (out["cv_dhw_ms"] * 1e-3) / 1e9
+    zimg = torch.randn((H, W), device="cuda") * 0.05
+    arms = ops.cbca_arms(zimg, 14, 0.02)
+    out["cbca_arms_ms"] = timeit(lambda: ops.cbca_arms(zimg, 14, 0.02, out=arms))
+    tmp = torch.empty_like(cvl)
+    out["cbca_1iter_ms"] = timeit(lambda: ops.cbca(cvl, arms, arms, "left", 14, 1, tmp=tmp))
+    # one iteration = horizontal pass (read C, write T) + vertical pass (read T, write C): 16 B/voxel
+    out["cbca_GBs_algorithmic"] = 16.0 * vox / (out["cbca_1iter_ms"] * 1e-3) / 1e9
+    out["cbca_1iter_L1_32_ms"] = timeit(lambda: ops.cbca(cvl, arms, arms, "left", 32, 1, tmp=tmp))
     print(json.dumps(out), flush=True)
 
 
