@@ -464,11 +464,16 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
 /*   referenced volume) or x + d (right-referenced); if o is outside the     */
 /*   image the support is {p}; else every arm is min(ref arm at p, other     */
 /*   arm at o).                                                              */
-/*  one iteration: horizontal pass T(p,d) = sum_{j=-hl..hr} C(y,x+j,d), then */
-/*   vertical pass C'(p,d) = (sum_{i=-vu..vd} T(y+i,x,d)) / cnt with cnt =   */
-/*   sum_i (hl+hr+1)(y+i, x, d): the mean over the union of the horizontal   */
-/*   segments hanging off p's vertical segment.  Sums are fp32, sequential   */
-/*   in ascending offset from 0.0f; cnt is exact; one IEEE fp32 division.    */
+/*  one iteration: horizontal pass, then vertical pass, each through an fp64  */
+/*   prefix sum accumulated sequentially from the start of the line:         */
+/*   P(x) = P(x-1) + (double)C(y,x,d), P(-1) = 0,                            */
+/*   T(p,d) = (float)(P(x+hr) - P(x-hl-1));                                  */
+/*   Q(y) = Q(y-1) + (double)T(y,x,d), Q(-1) = 0,                            */
+/*   C'(p,d) = (float)((Q(y+vd) - Q(y-vu-1)) / (double)cnt),                  */
+/*   cnt = sum_{i=-vu..vd} (hl+hr+1)(y+i, x, d) (exact integer): the mean    */
+/*   over the union of the horizontal segments hanging off p's vertical      */
+/*   segment.  (Prefix differences make each voxel O(1) on the GPU; fp64     */
+/*   keeps them accurate to ~1e-16 of the line sum.)                         */
 /* ------------------------------------------------------------------------ */
 EXPORT void sdeo_cbca_arms(const float *img, long pitch, int H, int W, int L1, float tau, uint32_t *arms)
 {
@@ -507,35 +512,45 @@ static inline void cbca_support(const uint32_t *ref, const uint32_t *oth, int W,
 EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
                             int D, int side)
 {
+    double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1));   /* P[x + 1] = prefix through x */
     for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++)
-            for (int d = 0; d < D; d++) {
+        for (int d = 0; d < D; d++) {
+            P[0] = 0.0;
+            for (int x = 0; x < W; x++) P[x + 1] = P[x] + (double)src[((size_t)y * W + x) * D + d];
+            for (int x = 0; x < W; x++) {
                 int a[4];
                 cbca_support(ref, oth, W, y, x, d, side, a);
-                float acc = 0.0f;
-                for (int j = -a[0]; j <= a[1]; j++) acc += src[((size_t)y * W + x + j) * D + d];
-                dst[((size_t)y * W + x) * D + d] = acc;
+                dst[((size_t)y * W + x) * D + d] = (float)(P[x + a[1] + 1] - P[x - a[0]]);
             }
+        }
+    free(P);
 }
 
 EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
                             int D, int side)
 {
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++)
-            for (int d = 0; d < D; d++) {
+    double *Q = (double *)malloc(sizeof(double) * (size_t)(H + 1));
+    long *N = (long *)malloc(sizeof(long) * (size_t)(H + 1));
+    for (int x = 0; x < W; x++)
+        for (int d = 0; d < D; d++) {
+            Q[0] = 0.0;
+            N[0] = 0;
+            for (int y = 0; y < H; y++) {
+                int b[4];
+                cbca_support(ref, oth, W, y, x, d, side, b);
+                Q[y + 1] = Q[y] + (double)src[((size_t)y * W + x) * D + d];
+                N[y + 1] = N[y] + b[0] + b[1] + 1;
+            }
+            for (int y = 0; y < H; y++) {
                 int a[4];
                 cbca_support(ref, oth, W, y, x, d, side, a);
-                float acc = 0.0f;
-                int cnt = 0;
-                for (int i = -a[2]; i <= a[3]; i++) {
-                    int b[4];
-                    cbca_support(ref, oth, W, y + i, x, d, side, b);
-                    acc += src[((size_t)(y + i) * W + x) * D + d];
-                    cnt += b[0] + b[1] + 1;
-                }
-                dst[((size_t)y * W + x) * D + d] = acc / (float)cnt;
+                const double num = Q[y + a[3] + 1] - Q[y - a[2]];
+                const long cnt = N[y + a[3] + 1] - N[y - a[2]];
+                dst[((size_t)y * W + x) * D + d] = (float)(num / (double)cnt);
             }
+        }
+    free(Q);
+    free(N);
 }
 
 /* iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv); result in cv. */

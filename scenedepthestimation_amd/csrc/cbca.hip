@@ -9,16 +9,17 @@
 // kernels reproduce it bit for bit (fp32 sums in ascending offset order from
 // 0.0f, exact integer counts, one IEEE division).
 //
-// Mapping.  One wave = one d-chunk of 64 disparities (lane = d, so every load
-// and store is a 256-B contiguous run of the HWD row) x one segment of NO
-// outputs along a line (a row for the horizontal pass, a column for the
-// vertical one).  The wave loads its NO + 2R window of cost rows into
-// registers once and forms every output as a masked, fixed-order sum over the
-// 2R + 1 taps, so each voxel is read from HBM about once (the halo hits L2:
-// the four waves of a workgroup take four consecutive segments of the same
-// line, and workgroups are remapped so neighbours share an XCD).  Arms of the
-// reference pixel are wave-uniform (scalar loads); the other image's arms at
-// x -/+ d are one coalesced 4-B gather per window row.
+// Mapping.  Both passes are line scans: one wave (one workgroup) walks one
+// line -- a row for the horizontal pass, a column for the vertical one -- for
+// one chunk of 64 disparities (lane = d, so each step moves one 256-B
+// contiguous run of the HWD volume).  The fp64 prefix sum P of the definition
+// is the wave's running state; the last 2R+2 prefixes live in a wave-private
+// LDS ring, so each output is two LDS reads at per-lane offsets (its own arms)
+// and one subtraction: O(1) work per voxel whatever the arm lengths.  The
+// output trails the front by R positions (its right/down arm is at most R).
+// Cost values and both images' arms are prefetched 8 positions ahead in a
+// register ring (unconditional, clamped loads), and the support arms of the
+// last R + 1 positions stay in registers for the trailing output.
 #include "sde_common.h"
 
 namespace sde {
@@ -46,117 +47,111 @@ __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict_
     arms[p] = packed;
 }
 
-__device__ __forceinline__ int xcd_remap_cb(int b, int nb)
+template <int R, bool VERT, int SIDE>
+__global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__ src, float *__restrict__ dst,
+                                                       const uint32_t *__restrict__ ref,
+                                                       const uint32_t *__restrict__ oth, int H, int W, int D)
 {
-    const int q = nb / 8, r = nb % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-// Support arms (l, r, u, d packed as bytes) of voxel (y, x, d): min of the
-// reference arms at x and the other image's arms at x -/+ d, or 0 outside.
-__device__ __forceinline__ uint32_t support(uint32_t a, const uint32_t *__restrict__ oth, size_t rowbase, int o,
-                                            int W, int R)
-{
-    if (o < 0 || o >= W) return 0u;
-    const uint32_t b = oth[rowbase + o];
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        int u = (a >> (8 * k)) & 255, v = (b >> (8 * k)) & 255;
-        u = u < v ? u : v;
-        u = u < R ? u : R;
-        s |= (uint32_t)u << (8 * k);
-    }
-    return s;
-}
-
-template <int R, int NO, bool VERT>
-__global__ __launch_bounds__(256) void cbca_pass_kernel(const float *__restrict__ src, float *__restrict__ dst,
-                                                        const uint32_t *__restrict__ ref,
-                                                        const uint32_t *__restrict__ oth, int H, int W, int D,
-                                                        int side, int nseg, int ndc)
-{
-    constexpr int NWIN = NO + 2 * R;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int ngrp = (nseg + 3) / 4;
-    const int lb = xcd_remap_cb(blockIdx.x, gridDim.x);
-    const int grp = lb % ngrp;
-    const int dc = (lb / ngrp) % ndc;
-    const int line = lb / (ngrp * ndc);
-    const int seg = grp * 4 + wave;
-    if (seg >= nseg) return;                       // wave-uniform; no barriers below
-    const int d = dc * 64 + lane;
-    const bool dok = d < D;
-    const int dl = dok ? d : D - 1;
-    const int len = VERT ? H : W;                  // positions along the line
-    const int p0 = seg * NO;
-    const int dsgn = side == SDE_SIDE_LEFT ? -1 : 1;
-
-    float v[NWIN];
-    uint32_t sup[VERT ? NWIN : 1];
-#pragma unroll
-    for (int t = 0; t < NWIN; t++) {
-        int q = p0 - R + t;
-        q = q < 0 ? 0 : (q >= len ? len - 1 : q);
-        const int y = VERT ? q : line, x = VERT ? line : q;
-        v[t] = src[((size_t)y * W + x) * D + dl];
-        if (VERT) {
-            const size_t rb = (size_t)y * W;
-            sup[t] = support(ref[rb + x], oth, rb, x + dsgn * d, W, R);
-        }
-    }
-#pragma unroll
-    for (int o = 0; o < NO; o++) {
-        const int q = p0 + o;
-        if (q < len) {
-            const int y = VERT ? q : line, x = VERT ? line : q;
-            uint32_t s;
-            if (VERT) {
-                s = sup[o + R];
-            } else {
-                const size_t rb = (size_t)y * W;
-                s = support(ref[rb + x], oth, rb, x + dsgn * d, W, R);
-            }
-            const int lo = VERT ? (s >> 16) & 255 : s & 255;           // up / left
-            const int hi = VERT ? (s >> 24) & 255 : (s >> 8) & 255;    // down / right
-            float acc = 0.0f;
-            int cnt = 0;
-#pragma unroll
-            for (int j = -R; j <= R; j++) {
-                const bool in = j < 0 ? (-j <= lo) : (j <= hi);
-                acc += in ? v[o + R + j] : 0.0f;
-                if (VERT) {
-                    const uint32_t sj = sup[o + R + j];
-                    cnt += in ? (int)((sj & 255) + ((sj >> 8) & 255) + 1) : 0;
-                }
-            }
-            if (dok) dst[((size_t)y * W + x) * D + d] = VERT ? acc / (float)cnt : acc;
-        }
-    }
-}
-
-template <int R, int NO, bool VERT>
-static void launch_pass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W, int D,
-                        int side, hipStream_t st)
-{
-    const int nlines = VERT ? W : H;
+    constexpr int RS = 2 * R + 2;      // prefix ring: positions [f - 2R - 1, f]; also the unroll
+    constexpr int U = R + 1;           // support ring (trailing output reads the slot of f - R)
+    constexpr int PF = 8;              // prefetch distance: 8 steps x 4 vector-memory ops < 63 (vmcnt)
+    static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && U % PF == 0, "ring sizes");
+    __shared__ double sP[RS * 64];
+    __shared__ int sN[VERT ? RS * 64 : 1];
+    const int lane = threadIdx.x;
+    // Lanes past D work on d = D-1: they compute lane D-1's value and store it to the
+    // same address, so no load, LDS access or store in the scan is predicated.
+    const int d = min((int)blockIdx.x * 64 + lane, D - 1);
+    const int line = blockIdx.y;
     const int len = VERT ? H : W;
-    const int nseg = (len + NO - 1) / NO;
-    const int ndc = (D + 63) / 64;
-    const int64_t nblk = (int64_t)nlines * ndc * ((nseg + 3) / 4);
-    cbca_pass_kernel<R, NO, VERT><<<(unsigned)nblk, 256, 0, st>>>(src, dst, ref, oth, H, W, D, side, nseg, ndc);
+    // opaque per-lane zero: keeps the (wave-uniform) reference-arm load a vector load,
+    // ordered under vmcnt with the rest of the ring instead of a scalar load whose
+    // out-of-order lgkmcnt (shared with the LDS ring) would serialise every step
+    const int vz = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    // vertical pass: the other pixel (line -/+ d) is fixed for the whole column
+    const int ov = SIDE == SDE_SIDE_LEFT ? line - d : line + d;
+    const bool vok = ov >= 0 && ov < W;
+    const int ovc = vok ? ov : 0;
+
+    float cr[PF];
+    uint32_t ar[PF], br[PF];
+    uint32_t sup[U];    // VERT: (up | down << 8) of the last U positions; else (left | right << 8)
+    auto issue = [&](int q, int slot) {
+        q = q < len ? q : len - 1;
+        const int y = VERT ? q : line, x = VERT ? line : q;
+        const size_t rb = (size_t)y * W;
+        cr[slot] = (src + (rb + x) * D)[d];
+        ar[slot] = (ref + rb + x)[vz];
+        int oc;
+        if (VERT) {
+            oc = ovc;
+        } else {
+            const int o = SIDE == SDE_SIDE_LEFT ? x - d : x + d;
+            oc = o < 0 ? 0 : (o >= W ? W - 1 : o);
+        }
+        br[slot] = (oth + rb)[oc];
+    };
+#pragma unroll
+    for (int j = 0; j < PF; j++) issue(j, j);
+#pragma unroll
+    for (int j = 0; j < U; j++) sup[j] = 0u;
+    double *const myP = sP + lane;
+    int *const myN = sN + (VERT ? lane : 0);
+    myP[(RS - 1) * 64] = 0.0;              // P(-1) = 0 (slot of position -1; rewritten at f = RS-1)
+    if (VERT) myN[(RS - 1) * 64] = 0;
+    double P = 0.0;
+    int N = 0;
+    for (int f0 = 0; f0 < len + R; f0 += RS) {
+#pragma unroll
+        for (int j = 0; j < RS; j++) {
+            const int f = f0 + j;
+            const int slot = j % PF;
+            const uint32_t a = ar[slot];
+            uint32_t b = br[slot];
+            if (VERT) {
+                b = vok ? b : 0u;                       // no other pixel: support {p}
+            } else {
+                const int x = f < len ? f : len - 1;
+                const bool ok = SIDE == SDE_SIDE_LEFT ? d <= x : d < W - x;
+                b = ok ? b : 0u;
+            }
+            const int l = min(a & 255, b & 255), r = min((a >> 8) & 255, (b >> 8) & 255);
+            // front: position f (positions >= len re-read the last one; never referenced)
+            P += (double)cr[slot];
+            myP[j * 64] = P;
+            if (VERT) {
+                N += l + r + 1;
+                myN[j * 64] = N;
+                sup[j % U] = min((a >> 16) & 255, (b >> 16) & 255) | (min(a >> 24, b >> 24) << 8);
+            } else {
+                sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
+            }
+            issue(f + PF, slot);
+            // trailing output y = f - R; its support arms from the ring slot of position y
+            const int y = f - R;
+            if (y >= 0 && y < len) {
+                const uint32_t sy = sup[(j + 1) % U];
+                const int lo = sy & 255, hi = sy >> 8;
+                const int ib = ((j - R + hi) & (RS - 1)) * 64, ia = ((j - R - lo - 1) & (RS - 1)) * 64;
+                const double pb = myP[ib], pa = myP[ia];
+                float out;
+                if (VERT) out = (float)((pb - pa) / (double)(myN[ib] - myN[ia]));
+                else out = (float)(pb - pa);
+                const int yy = VERT ? y : line, xx = VERT ? line : y;
+                (dst + ((size_t)yy * W + xx) * D)[d] = out;
+            }
+        }
+    }
 }
 
-// NOH / NOV: outputs per wave of the horizontal / vertical pass (the vertical
-// pass also keeps every window row's support arms, so it takes shorter segments
-// to stay fully unrolled in registers).
-template <int R, int NOH, int NOV>
-static void cbca_iters(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D, int side,
+template <int R, int SIDE>
+static void cbca_iters(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D,
                        int iters, hipStream_t st)
 {
+    const int ndc = (D + 63) / 64;
     for (int it = 0; it < iters; it++) {
-        launch_pass<R, NOH, false>(cv, tmp, ref, oth, H, W, D, side, st);
-        launch_pass<R, NOV, true>(tmp, cv, ref, oth, H, W, D, side, st);
+        cbca_scan_kernel<R, false, SIDE><<<dim3(ndc, H), 64, 0, st>>>(cv, tmp, ref, oth, H, W, D);
+        cbca_scan_kernel<R, true, SIDE><<<dim3(ndc, W), 64, 0, st>>>(tmp, cv, ref, oth, H, W, D);
     }
 }
 
@@ -178,9 +173,14 @@ SDE_EXPORT int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const u
     if (!cv || !tmp || !arms_ref || !arms_other || H <= 0 || W <= 0 || D <= 0 || iters < 0 || L1 < 1 ||
         L1 > SDE_CBCA_MAX_L1 || (side != SDE_SIDE_LEFT && side != SDE_SIDE_RIGHT) || cv == tmp)
         return SDE_ERR_ARG;
-    if ((int64_t)H * W * ((D + 63) / 64) > ((int64_t)1 << 31) * 16) return SDE_ERR_ARG;
+    if (H > 65535 || W > 65535) return SDE_ERR_ARG;      // grid.y = lines
     hipStream_t st = as_stream(stream);
-    if (L1 <= 16) cbca_iters<15, 32, 16>(cv, tmp, arms_ref, arms_other, H, W, D, side, iters, st);
-    else cbca_iters<31, 16, 8>(cv, tmp, arms_ref, arms_other, H, W, D, side, iters, st);
+    if (side == SDE_SIDE_LEFT) {
+        if (L1 <= 16) cbca_iters<15, SDE_SIDE_LEFT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
+        else cbca_iters<31, SDE_SIDE_LEFT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
+    } else {
+        if (L1 <= 16) cbca_iters<15, SDE_SIDE_RIGHT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
+        else cbca_iters<31, SDE_SIDE_RIGHT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
+    }
     return launch_status();
 }

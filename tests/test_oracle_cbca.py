@@ -42,24 +42,24 @@ def cbca_literal(cv, ref, oth, side, iters):
     for _ in range(iters):
         T = np.zeros_like(cur)
         for y in range(H):
-            for x in range(W):
-                for d in range(D):
+            for d in range(D):
+                P = [0.0]
+                for x in range(W):
+                    P.append(P[-1] + float(cur[y, x, d]))          # Python float = IEEE fp64
+                for x in range(W):
                     a = support(ref, oth, y, x, d, side)
-                    acc = np.float32(0.0)
-                    for j in range(-a[0], a[1] + 1):
-                        acc = np.float32(acc + cur[y, x + j, d])
-                    T[y, x, d] = acc
+                    T[y, x, d] = np.float32(P[x + a[1] + 1] - P[x - a[0]])
         nxt = np.zeros_like(cur)
-        for y in range(H):
-            for x in range(W):
-                for d in range(D):
+        for x in range(W):
+            for d in range(D):
+                Q, N = [0.0], [0]
+                for y in range(H):
+                    b = support(ref, oth, y, x, d, side)
+                    Q.append(Q[-1] + float(T[y, x, d]))
+                    N.append(N[-1] + b[0] + b[1] + 1)
+                for y in range(H):
                     a = support(ref, oth, y, x, d, side)
-                    acc, cnt = np.float32(0.0), 0
-                    for i in range(-a[2], a[3] + 1):
-                        b = support(ref, oth, y + i, x, d, side)
-                        acc = np.float32(acc + T[y + i, x, d])
-                        cnt += b[0] + b[1] + 1
-                    nxt[y, x, d] = np.float32(acc / np.float32(cnt))
+                    nxt[y, x, d] = np.float32((Q[y + a[3] + 1] - Q[y - a[2]]) / float(N[y + a[3] + 1] - N[y - a[2]]))
         cur = nxt
     return cur
 
@@ -96,11 +96,12 @@ def test_cbca_properties():
     H, W, D = 12, 17, 6
     cv = rng.standard_normal((H, W, D)).astype(np.float32)
     flat = np.zeros((H, W), np.float32)
-    zero = oracle.cbca_arms(flat, 14, 0.0)                 # tau = 0: no arms -> identity
-    assert oracle.cbca(cv, zero, zero, "left", 3).tobytes() == cv.tobytes()
+    zero = oracle.cbca_arms(flat, 14, 0.0)                 # tau = 0: no arms -> identity (up to the prefix
+    np.testing.assert_allclose(oracle.cbca(cv, zero, zero, "left", 3), cv, rtol=1e-7, atol=1e-12)  # rounding)
+    assert oracle.cbca(cv, zero, zero, "left", 0).tobytes() == cv.tobytes()
     full = oracle.cbca_arms(flat, 64, 1.0)                 # flat image, long arms: support = whole image
     out = oracle.cbca(cv, full, full, "left", 1)
     for d in range(D):
         # left-referenced: voxels with x >= d average over the region x' >= d; x < d stays as is
         np.testing.assert_allclose(out[:, d:, d], cv[:, d:, d].mean(), rtol=2e-5, atol=2e-6)
-        assert out[:, :d, d].tobytes() == cv[:, :d, d].tobytes()
+        np.testing.assert_allclose(out[:, :d, d], cv[:, :d, d], rtol=1e-7, atol=1e-12)
