@@ -54,8 +54,8 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
 {
     constexpr int RS = 2 * R + 2;      // prefix ring: positions [f - 2R - 1, f]; also the unroll
     constexpr int U = R + 1;           // support ring (trailing output reads the slot of f - R)
-    constexpr int PF = 8;              // prefetch distance: 8 steps x 4 vector-memory ops < 63 (vmcnt)
-    static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && U % PF == 0, "ring sizes");
+    constexpr int PF = 16;             // prefetch distance (vmcnt saturates at 63 outstanding ops)
+    static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && RS % PF == 0, "ring sizes");
     __shared__ double sP[RS * 64];
     __shared__ int sN[VERT ? RS * 64 : 1];
     const int lane = threadIdx.x;
@@ -68,79 +68,86 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     // ordered under vmcnt with the rest of the ring instead of a scalar load whose
     // out-of-order lgkmcnt (shared with the LDS ring) would serialise every step
     const int vz = __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    // per-position strides (elements) and per-line bases: position q of this line is
+    // src/dst + cbase + q*cstride, ref + abase + q*astride, oth + abase + q*astride + o(q)
+    const int cstride = VERT ? W * D : D, astride = VERT ? W : 1;
+    const size_t cbase = VERT ? (size_t)line * D : (size_t)line * W * D;
+    const size_t abase = VERT ? (size_t)line : (size_t)line * W;
     // vertical pass: the other pixel (line -/+ d) is fixed for the whole column
     const int ov = SIDE == SDE_SIDE_LEFT ? line - d : line + d;
     const bool vok = ov >= 0 && ov < W;
-    const int ovc = vok ? ov : 0;
+    const int ovc = (vok ? ov : 0) - line;          // offset from the reference pixel
 
+    double P_acc = 0.0;
+    int N_acc = 0;
     float cr[PF];
     uint32_t ar[PF], br[PF];
     uint32_t sup[U];    // VERT: (up | down << 8) of the last U positions; else (left | right << 8)
     auto issue = [&](int q, int slot) {
-        q = q < len ? q : len - 1;
-        const int y = VERT ? q : line, x = VERT ? line : q;
-        const size_t rb = (size_t)y * W;
-        cr[slot] = (src + (rb + x) * D)[d];
-        ar[slot] = (ref + rb + x)[vz];
-        int oc;
+        const float *pc = src + cbase + (size_t)q * cstride;
+        const uint32_t *pa = ref + abase + (size_t)q * astride;
+        cr[slot] = pc[d];
+        ar[slot] = pa[vz];
+        int oo;
         if (VERT) {
-            oc = ovc;
+            oo = ovc;
         } else {
-            const int o = SIDE == SDE_SIDE_LEFT ? x - d : x + d;
-            oc = o < 0 ? 0 : (o >= W ? W - 1 : o);
+            const int o = SIDE == SDE_SIDE_LEFT ? q - d : q + d;
+            oo = (o < 0 ? 0 : (o >= W ? W - 1 : o)) - q;
         }
-        br[slot] = (oth + rb)[oc];
+        br[slot] = pa[oo + (oth - ref)];
+    };
+    auto step = [&](int j, int f, bool tail) {
+        const int slot = j % PF;
+        const uint32_t a = ar[slot];
+        uint32_t b = br[slot];
+        if (VERT) {
+            b = vok ? b : 0u;                       // no other pixel: support {p}
+        } else {
+            const int x = tail ? (f < len ? f : len - 1) : f;
+            const bool ok = SIDE == SDE_SIDE_LEFT ? d <= x : d < W - x;
+            b = ok ? b : 0u;
+        }
+        const int l = min(a & 255, b & 255), r = min((a >> 8) & 255, (b >> 8) & 255);
+        // front: position f (tail positions >= len re-read the last one; never referenced)
+        P_acc += (double)cr[slot];
+        sP[j * 64 + lane] = P_acc;
+        if (VERT) {
+            N_acc += l + r + 1;
+            sN[j * 64 + lane] = N_acc;
+            sup[j % U] = min((a >> 16) & 255, (b >> 16) & 255) | (min(a >> 24, b >> 24) << 8);
+        } else {
+            sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
+        }
+        issue(tail ? min(f + PF, len - 1) : f + PF, slot);
+        // trailing output y = f - R; its support arms from the ring slot of position y
+        const int y = f - R;
+        if (y >= 0 && (!tail || y < len)) {
+            const uint32_t sy = sup[(j + 1) % U];
+            const int lo = sy & 255, hi = sy >> 8;
+            const int ib = ((j - R + hi) & (RS - 1)) * 64 + lane, ia = ((j - R - lo - 1) & (RS - 1)) * 64 + lane;
+            const double pb = sP[ib], pa = sP[ia];
+            float out;
+            if (VERT) out = (float)((pb - pa) / (double)(sN[ib] - sN[ia]));
+            else out = (float)(pb - pa);
+            (dst + cbase + (size_t)y * cstride)[d] = out;
+        }
     };
 #pragma unroll
-    for (int j = 0; j < PF; j++) issue(j, j);
+    for (int j = 0; j < PF; j++) issue(min(j, len - 1), j);
 #pragma unroll
     for (int j = 0; j < U; j++) sup[j] = 0u;
-    double *const myP = sP + lane;
-    int *const myN = sN + (VERT ? lane : 0);
-    myP[(RS - 1) * 64] = 0.0;              // P(-1) = 0 (slot of position -1; rewritten at f = RS-1)
-    if (VERT) myN[(RS - 1) * 64] = 0;
-    double P = 0.0;
-    int N = 0;
-    for (int f0 = 0; f0 < len + R; f0 += RS) {
+    sP[(RS - 1) * 64 + lane] = 0.0;        // P(-1) = 0 (slot of position -1; rewritten at f = RS-1)
+    if (VERT) sN[(RS - 1) * 64 + lane] = 0;
+    int f0 = 0;
+    // main blocks: every prefetched position is inside the line (no clamps)
+    for (; f0 + RS + PF <= len; f0 += RS) {
 #pragma unroll
-        for (int j = 0; j < RS; j++) {
-            const int f = f0 + j;
-            const int slot = j % PF;
-            const uint32_t a = ar[slot];
-            uint32_t b = br[slot];
-            if (VERT) {
-                b = vok ? b : 0u;                       // no other pixel: support {p}
-            } else {
-                const int x = f < len ? f : len - 1;
-                const bool ok = SIDE == SDE_SIDE_LEFT ? d <= x : d < W - x;
-                b = ok ? b : 0u;
-            }
-            const int l = min(a & 255, b & 255), r = min((a >> 8) & 255, (b >> 8) & 255);
-            // front: position f (positions >= len re-read the last one; never referenced)
-            P += (double)cr[slot];
-            myP[j * 64] = P;
-            if (VERT) {
-                N += l + r + 1;
-                myN[j * 64] = N;
-                sup[j % U] = min((a >> 16) & 255, (b >> 16) & 255) | (min(a >> 24, b >> 24) << 8);
-            } else {
-                sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
-            }
-            issue(f + PF, slot);
-            // trailing output y = f - R; its support arms from the ring slot of position y
-            const int y = f - R;
-            if (y >= 0 && y < len) {
-                const uint32_t sy = sup[(j + 1) % U];
-                const int lo = sy & 255, hi = sy >> 8;
-                const int ib = ((j - R + hi) & (RS - 1)) * 64, ia = ((j - R - lo - 1) & (RS - 1)) * 64;
-                const double pb = myP[ib], pa = myP[ia];
-                float out;
-                if (VERT) out = (float)((pb - pa) / (double)(myN[ib] - myN[ia]));
-                else out = (float)(pb - pa);
-                const int yy = VERT ? y : line, xx = VERT ? line : y;
-                (dst + ((size_t)yy * W + xx) * D)[d] = out;
-            }
-        }
+        for (int j = 0; j < RS; j++) step(j, f0 + j, false);
+    }
+    for (; f0 < len + R; f0 += RS) {
+#pragma unroll
+        for (int j = 0; j < RS; j++) step(j, f0 + j, true);
     }
 }
 
