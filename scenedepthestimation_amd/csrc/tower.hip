@@ -586,14 +586,14 @@ static void set_tower_attrs()
 {
     static bool done = false;
     if (done) return;
-    hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-    hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-    hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-    hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-    hipFuncSetAttribute((const void *)conv64_x6_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    hipFuncSetAttribute((const void *)conv64_x6_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    hipFuncSetAttribute((const void *)conv64_x6_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    hipFuncSetAttribute((const void *)conv64_x6_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
     done = true;
 }
 
