@@ -44,13 +44,32 @@ WORKLOADS = {
     "north_star": (1024, 1024, 192, "tower+cv_wta"),
     "cones": (375, 450, 64, "tower+cv_wta"),
     "cv": (1024, 1024, 192, "cv_wta"),
+    # BASELINE config 3: Middlebury-2014 full-resolution scale, D = 256, cross-based aggregation + SGM
+    "c3": (2000, 3000, 256, "tower+cbca+sgm"),
+    # the north-star size through the reference's whole GPU path (+ the build-defined CBCA)
+    "north_star_sgm": (1024, 1024, 192, "tower+cbca+sgm"),
 }
+CBCA_ITERS, CBCA_L1, CBCA_TAU = 2, 14, 0.02
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
 PEAK_BF16_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
 PEAK_VALU_F32_TOPS = 78.6     # non-fused f32 ops/s (one op per lane-slot; FMA counts 2 in the 157.3)
 NF = 64
 NLAYERS = 5
+
+
+def measured_traffic(workload):
+    """HBM bytes per launch of this workload's dominant kernel, from the newest committed PMC summary
+    (profiles/rNN/traffic.json, written by tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            entry = json.load(open(f)).get(workload)
+        except (OSError, ValueError):
+            continue
+        if entry:
+            return entry["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def conv_flops(hout, wout):
@@ -114,6 +133,19 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
             t_tower.stop(e_t)
         m.split_valid = m.split is not None
 
+    if what == "tower+cbca+sgm":
+        def step_sgm(timed=False):
+            e = t_tower.start() if timed else None
+            m.features()
+            if e is not None:
+                t_tower.stop(e)
+            e = t_cv.start() if timed else None
+            out = m.sgm_path(post=True)
+            if e is not None:
+                t_cv.stop(e)
+            return out
+        return step_sgm
+
     def step(timed=False):
         if what == "tower+cv_wta":
             tower(0, timed)
@@ -151,6 +183,35 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
         oracle.cv_wta_shard(fl, fr, 0, D)
         return time.perf_counter() - t0
 
+    if what == "tower+cbca+sgm":
+        # SGM's vertical and diagonal paths need whole columns: time a crop of the same workload
+        # (rows x cols of the same pair, full D) through tower + L/R cost volume + CBCA + 8-path SGM
+        # (both sides) + WTA + LR check + LRC + median, and scale per voxel.
+        def run_crop(hc, wc):
+            t0 = time.perf_counter()
+            feats, zs = [], []
+            for img in (left, right):
+                crop = img[:hc, :wc]
+                z = oracle.znorm(crop.astype(np.float32))
+                zs.append(z)
+                feats.append(oracle.tower_forward(oracle.pad_image(z, 2 * NLAYERS + 1), hw, hb))
+            cl, cr = oracle.cost_volume_hwd(feats[0], feats[1], D, invalid=1.0, right=True)
+            al, ar = oracle.cbca_arms(zs[0], CBCA_L1, CBCA_TAU), oracle.cbca_arms(zs[1], CBCA_L1, CBCA_TAU)
+            cl = oracle.cbca(cl, al, ar, "left", CBCA_ITERS)
+            cr = oracle.cbca(cr, ar, al, "right", CBCA_ITERS)
+            dl = oracle.wta_sgm(oracle.sgm_8path(cl, oracle.sgm_penalties(left[:hc, :wc])))
+            dr = oracle.wta_sgm(oracle.sgm_8path(cr, oracle.sgm_penalties(right[:hc, :wc])))
+            a, _ = oracle.lr_check(dl, dr)
+            oracle.median5(oracle.lrc_fill(dl, a))
+            return time.perf_counter() - t0
+        hc, wc = 16, max(D + 16, 64)
+        t1 = run_crop(hc, wc)
+        hc = int(max(16, min(H, hc * budget_s / max(t1, 1e-6))))
+        t = run_crop(hc, wc)
+        return {"value": hc * wc * D / t / 1e6, "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
+                "sample": f"{hc} x {wc} crop x D={D} of the {H}x{W} pair through the full GPU path restated in C "
+                          f"(fp64 tower, L/R cost volume, CBCA x{CBCA_ITERS}, 8-path SGM both sides, WTA, LR check, "
+                          f"LRC, median), {t:.1f} s"}
     t1 = run(1)
     rows = int(max(1, min(H, budget_s / max(t1, 1e-6))))
     t = run(rows)
@@ -191,7 +252,9 @@ def main():
             return r
         pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
     else:
-        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
+        sgm = what == "tower+cbca+sgm"
+        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode, sgm=sgm,
+                          cbca_iters=CBCA_ITERS if sgm else 0, cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
         m.load_images(left, right)
         if what == "cv_wta":
             m.features()
@@ -223,7 +286,38 @@ def main():
 
     roof = None
     stages = {}
-    if args.mode == "pairdp" or world == 1:
+    if what == "tower+cbca+sgm" and (args.mode == "pairdp" or world == 1):
+        stages["tower_ms_pair"] = t_tower.mean_ms()
+        stages["gpu_path_ms"] = t_cv.mean_ms()
+        tim = {}
+        m.sgm_path(post=True, timings=tim)           # one synchronised pass, per-stage wall times
+        stages.update({f"{k}_ms": v * 1e3 for k, v in tim.items()})
+        b = m.sgm_bufs
+        # the SGM pair (both sides, 8 directions = 8 launches) timed alone with HIP events
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.sgm_8path_pair(b["cv"][0], b["pen"][0], b["S"][0], b["cv"][1], b["pen"][1], b["S"][1])
+        e1.record()
+        torch.cuda.synchronize()
+        sgm_ms = e0.elapsed_time(e1)
+        sgm_bytes = 2 * 92.0 * vox          # per side: 8 B/voxel (first direction) + 7 x 12 B/voxel
+        tmp = b["cbca_tmp"]
+        e0.record()
+        ops.cbca(b["cv"][0], b["arms"][0], b["arms"][1], "left", CBCA_L1, 1, tmp=tmp)
+        e1.record()
+        torch.cuda.synchronize()
+        cb_ms = e0.elapsed_time(e1)
+        stages["cbca_iter_ms"] = cb_ms
+        stages["cbca_iter_hbm_GBs"] = 16.0 * vox / (cb_ms * 1e-3) / 1e9     # 2 passes x (read + write) x 4 B
+        stages["sgm_pair_ms"] = sgm_ms
+        ach = sgm_bytes / (sgm_ms * 1e-3) / 1e9
+        roof = {"kernel": "sgm_scan_kernel (8-path SGM, both sides, 8 launches)", "bound": "hbm",
+                "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                "traffic": None,
+                "per_launch": f"2 sides x (8 + 7 x 12) B/voxel x {vox / 1e6:.0f} Mvox = {sgm_bytes / 1e9:.2f} GB "
+                              f"over {sgm_ms:.3f} ms (8 launches)"}
+    elif args.mode == "pairdp" or world == 1:
         cv_ms = t_cv.mean_ms()
         bytes_cv = 4.0 * H * W * 2 * NF + 4.0 * H * W
         stages["cv_wta_ms"] = cv_ms
@@ -272,6 +366,12 @@ def main():
                                   f"VALU {stages['cv_wta_valu_frac']:.2f} of {PEAK_VALU_F32_TOPS} Top/s"}
     else:
         stages["dshard_step_ms"] = t_tower.mean_ms()
+
+    if roof is not None:
+        tb, src = measured_traffic(args.workload)
+        roof["traffic"] = tb
+        roof["traffic_unit"] = "bytes per launch (HBM, PMC)"
+        roof["traffic_source"] = src
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
