@@ -202,7 +202,7 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
             dl = oracle.wta_sgm(oracle.sgm_8path(cl, oracle.sgm_penalties(left[:hc, :wc])))
             dr = oracle.wta_sgm(oracle.sgm_8path(cr, oracle.sgm_penalties(right[:hc, :wc])))
             a, _ = oracle.lr_check(dl, dr)
-            oracle.median5(oracle.lrc_fill(dl, a))
+            oracle.median5(oracle.lrc_fill(dl, a), dl)
             return time.perf_counter() - t0
         hc, wc = 16, max(D + 16, 64)
         t1 = run_crop(hc, wc)

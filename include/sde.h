@@ -249,7 +249,9 @@ int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *ar
 int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,
                  void *stream);
 
-/* LRC_kernel left output (process_functional.py:1003-1088). */
+/* LRC_kernel left output (process_functional.py:1003-1088).  Two linear scans instead of
+ * the reference's per-pixel walks; `out` doubles as scratch, so out != disp_l.  Requires
+ * H < 65535 and W <= 4096. */
 int sde_lrc_fill(const float *disp_l, const uint8_t *lrc_l, int H, int W, float *out, void *stream);
 
 /* Median_Filter_kernel (process_functional.py:840-879): 5x5 median of src into the interior of dst. */

@@ -367,28 +367,114 @@ __global__ __launch_bounds__(256) void lr_check_kernel(const float *__restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void lrc_fill_kernel(const float *__restrict__ dl, const uint8_t *__restrict__ f,
-                                                       int H, int W, float *__restrict__ out)
+// LRC_kernel (:1003-1088): every flagged pixel takes the mean of the nearest unflagged
+// pixel above, below, to the right and to the left (each only if it exists), summed in
+// that order in float64.  The reference walks each direction pixel by pixel, which is
+// quadratic in the length of a flagged run; here linear scans find the same four
+// pixels.  Pass 1 (wave per column): nearest unflagged row above / below of every
+// flagged pixel, parked in the output as two 16-bit row indices (0xFFFF = none).
+// Pass 2 (wave per row): nearest unflagged column to the left (sweep left -> right) and
+// to the right (sweep right -> left) by wave-wide max-scans over 64-pixel chunks; the
+// right sweep, which runs second, has all four neighbours and writes the result.
+constexpr uint32_t LRC_NONE = 0xFFFFu;
+
+// inclusive max-scan over the 64 lanes
+__device__ __forceinline__ int wave_max_scan(int v)
 {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= (int64_t)H * W) return;
-    const int y = (int)(p / W), x = (int)(p % W);
-    if (f[p] != 1) { out[p] = dl[p]; return; }
-    int number = 0;
-    double sum = 0.0;
-    int iy = y;
-    while (iy >= 0 && f[(size_t)iy * W + x] == 1) iy--;
-    if (iy >= 0) { number++; sum += dl[(size_t)iy * W + x]; }
-    iy = y;
-    while (iy < H && f[(size_t)iy * W + x] == 1) iy++;
-    if (iy < H) { number++; sum += dl[(size_t)iy * W + x]; }
-    int ix = x;
-    while (ix < W && f[(size_t)y * W + ix] == 1) ix++;
-    if (ix < W) { number++; sum += dl[(size_t)y * W + ix]; }
-    ix = x;
-    while (ix >= 0 && f[(size_t)y * W + ix] == 1) ix--;
-    if (ix >= 0) { number++; sum += dl[(size_t)y * W + ix]; }
-    out[p] = number > 0 ? (float)(sum / number) : dl[p];
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v = v > t ? v : t;
+    }
+    return v;
+}
+
+// Pass 1: one wave per column, 64 rows per step, wave-wide max-scans downwards (nearest
+// unflagged row above, strictly) and upwards (below), carried across chunks.
+__global__ __launch_bounds__(64) void lrc_cols_kernel(const uint8_t *__restrict__ f, int H, int W,
+                                                      uint32_t *__restrict__ park)
+{
+    const int x = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int nchunk = (H + 63) / 64;
+    int carry = -1;
+    for (int c = 0; c < nchunk; c++) {             // top -> bottom
+        const int y = c * 64 + lane;
+        const bool in = y < H;
+        const bool flagged = in && f[(size_t)y * W + x] == 1;
+        const int v = wave_max_scan(in && !flagged ? y : -1);
+        int prev = __shfl_up(v, 1, 64);
+        if (lane == 0) prev = -1;
+        const int up = prev > carry ? prev : carry;
+        const int last = __builtin_amdgcn_readlane(v, 63);
+        carry = last > carry ? last : carry;
+        if (flagged) park[(size_t)y * W + x] = up < 0 ? LRC_NONE : (uint32_t)up;
+    }
+    carry = -1;                                    // as H-1-y of the nearest unflagged row below
+    for (int c = 0; c < nchunk; c++) {             // bottom -> top
+        const int y = H - 1 - (c * 64 + lane);
+        const bool in = y >= 0;
+        const bool flagged = in && f[(size_t)(in ? y : 0) * W + x] == 1;
+        const int v = wave_max_scan(in && !flagged ? H - 1 - y : -1);
+        int prev = __shfl_up(v, 1, 64);
+        if (lane == 0) prev = -1;
+        const int dn = prev > carry ? prev : carry;
+        const int last = __builtin_amdgcn_readlane(v, 63);
+        carry = last > carry ? last : carry;
+        if (flagged) park[(size_t)y * W + x] |= (dn < 0 ? LRC_NONE : (uint32_t)(H - 1 - dn)) << 16;
+    }
+}
+
+__global__ __launch_bounds__(64) void lrc_rows_kernel(const float *__restrict__ dl, const uint8_t *__restrict__ f,
+                                                      int H, int W, float *__restrict__ out)
+{
+    __shared__ int16_t sleft[4096];                // nearest unflagged column left of x (-1 = none)
+    const int y = blockIdx.x;
+    const int lane = threadIdx.x;
+    const size_t row = (size_t)y * W;
+    const uint32_t *park = reinterpret_cast<const uint32_t *>(out);
+    const int nchunk = (W + 63) / 64;
+    int carry = -1;
+    for (int c = 0; c < nchunk; c++) {             // left -> right
+        const int x = c * 64 + lane;
+        const bool in = x < W;
+        const bool clear = in && f[row + x] != 1;
+        const int v = wave_max_scan(clear ? x : -1);
+        int prev = __shfl_up(v, 1, 64);
+        if (lane == 0) prev = -1;
+        if (in) sleft[x] = (int16_t)(prev > carry ? prev : carry);
+        const int last = __builtin_amdgcn_readlane(v, 63);
+        carry = last > carry ? last : carry;
+    }
+    __syncthreads();
+    carry = -1;                                    // as W-1-x of the nearest unflagged column to the right
+    for (int c = 0; c < nchunk; c++) {             // right -> left
+        const int x = W - 1 - (c * 64 + lane);
+        const bool in = x >= 0;
+        const bool flagged = in && f[row + x] == 1;
+        const int v = wave_max_scan(in && !flagged ? W - 1 - x : -1);
+        int prev = __shfl_up(v, 1, 64);
+        if (lane == 0) prev = -1;
+        const int rr = prev > carry ? prev : carry;
+        const int last = __builtin_amdgcn_readlane(v, 63);
+        carry = last > carry ? last : carry;
+        if (!in) continue;
+        if (!flagged) {
+            out[row + x] = dl[row + x];
+            continue;
+        }
+        const uint32_t pk = park[row + x];
+        const uint32_t up = pk & 0xFFFFu, down = pk >> 16;
+        const int left = sleft[x];
+        int number = 0;
+        double sum = 0.0;
+        if (up != LRC_NONE) { number++; sum += dl[(size_t)up * W + x]; }
+        if (down != LRC_NONE) { number++; sum += dl[(size_t)down * W + x]; }
+        if (rr >= 0) { number++; sum += dl[row + (W - 1 - rr)]; }
+        if (left >= 0) { number++; sum += dl[row + left]; }
+        out[row + x] = number > 0 ? (float)(sum / number) : dl[row + x];
+    }
 }
 
 __global__ __launch_bounds__(256) void median5_kernel(const float *__restrict__ src, int H, int W,
@@ -473,7 +559,10 @@ SDE_EXPORT int sde_lr_check(const float *disp_l, const float *disp_r, int H, int
 SDE_EXPORT int sde_lrc_fill(const float *disp_l, const uint8_t *lrc_l, int H, int W, float *out, void *stream)
 {
     if (!disp_l || !lrc_l || !out || H <= 0 || W <= 0) return SDE_ERR_ARG;
-    lrc_fill_kernel<<<cdiv((int64_t)H * W, 256), 256, 0, as_stream(stream)>>>(disp_l, lrc_l, H, W, out);
+    if (H >= (int)LRC_NONE || W > 4096 || out == disp_l) return SDE_ERR_ARG;   // 16-bit rows, LDS row
+    hipStream_t st = as_stream(stream);
+    lrc_cols_kernel<<<W, 64, 0, st>>>(lrc_l, H, W, reinterpret_cast<uint32_t *>(out));
+    lrc_rows_kernel<<<H, 64, 0, st>>>(disp_l, lrc_l, H, W, out);
     return launch_status();
 }
 

@@ -110,6 +110,7 @@ def disparity_compute_by_gpu(imagel, imager, featuresl, featuresr, detail_time, 
     m = StereoMatcher.__new__(StereoMatcher)
     m.H, m.W, m.D, m.device = H, W, int(ndisp), fl.device
     m.sgm_bufs = None
+    m.cbca_iters = 0          # the reference has no aggregation stage
     timings = {}
     dl, dr = m.sgm_path(fl=fl, fr=fr, img_l=il, img_r=ir, timings=timings)
     for slot, key in ((1, "cost_volume"), (3, "sgm"), (4, "wta"), (5, "lrc"), (6, "filter")):

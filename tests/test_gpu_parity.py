@@ -283,6 +283,19 @@ def test_matcher_cbca_sgm_end_to_end(gpu, oracle):
     assert np.array_equal(host(dr), oracle.wta_sgm(Sr))
 
 
+@pytest.mark.parametrize("H,W,frac", [(37, 300, 0.9), (5, 4096, 0.5), (64, 129, 1.0), (64, 129, 0.0),
+                                       (300, 70, 0.97)])
+def test_lrc_fill_runs_bit_exact(gpu, oracle, H, W, frac):
+    """Long flagged runs (quadratic for the reference's walks), fully flagged and clean maps."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(H * W)
+    dl = rng.integers(0, 60, (H, W)).astype(np.float32) + rng.random((H, W)).astype(np.float32)
+    flags = (rng.random((H, W)) < frac).astype(np.uint8)
+    flags[H // 2, :] = 1                      # a whole flagged row and column
+    flags[:, W // 3] = 1
+    assert host(ops.lrc_fill(dev(dl), dev(flags))).tobytes() == oracle.lrc_fill(dl, flags).tobytes()
+
+
 def test_post_processing_bit_exact(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(12)
