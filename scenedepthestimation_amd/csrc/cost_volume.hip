@@ -31,7 +31,7 @@ constexpr int CV_DC = 64;                    // disparities per LDS chunk
 constexpr int CV_DW = CV_DC / CV_WAVES;      // disparities per wave per chunk
 constexpr int CV_ROWS = CV_TX + CV_DC - 1;   // other-side rows per chunk
 
-enum { OUT_WTA = 0, OUT_DHW = 1, OUT_HWD = 2 };
+enum { OUT_WTA = 0, OUT_DHW = 1, OUT_HWD = 2, OUT_HWD_LR = 3 };
 
 // Exact -(0 + pairwise8) of own[64] (registers) and one swizzled LDS row.
 __device__ __forceinline__ float dot64_exact(const float (&own)[64], const float4 *__restrict__ win, int lr)
@@ -59,15 +59,21 @@ __device__ __forceinline__ float dot64_exact(const float (&own)[64], const float
 
 // SIDE_LEFT : own = fl at x,  other = fr at x - d   (L[y][x][d])
 // SIDE_RIGHT: own = fr at x', other = fl at x' + d  (R[y][x'][d] = cost(x'+d, d))
+// OUT_HWD_LR (SIDE_LEFT only): every voxel is computed once and stored twice,
+// L[y][q][d] and R[y][q-d][d] (the right volume is the left one sheared, bit for bit:
+// the products commute and the channel order is the same).  The grid runs D-1 pixels
+// past the row end so the blocks owning q >= W write R's invalid fill.
 template <int SIDE, int OUT>
 __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own_feat,
                                                    const float *__restrict__ other_feat, int H, int W,
                                                    int d0, int d1, int Dvol, float invalid,
                                                    float *__restrict__ out, float *__restrict__ out_min,
-                                                   int32_t *__restrict__ out_arg, float *__restrict__ out_disp)
+                                                   int32_t *__restrict__ out_arg, float *__restrict__ out_disp,
+                                                   float *__restrict__ out_r)
 {
+    constexpr bool TILE = OUT == OUT_HWD || OUT == OUT_HWD_LR;
     __shared__ float4 win[CV_ROWS * 16];
-    __shared__ float otile[OUT == OUT_HWD ? CV_TX * (CV_DC + 1) : 1];
+    __shared__ float otile[TILE ? CV_TX * (CV_DC + 1) : 1];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -114,12 +120,22 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
                 otile[lane * (CV_DC + 1) + (d - dc)] = cost;
             }
         }
-        if (OUT == OUT_HWD) {
+        if (TILE) {
             __syncthreads();
             const int nd = dce - dc;
             for (int i = wave; i < CV_TX; i += CV_WAVES) {
                 if (q0 + i < W && lane < nd)
                     out[((size_t)y * W + q0 + i) * Dvol + dc + lane] = otile[i * (CV_DC + 1) + lane];
+            }
+        }
+        if (OUT == OUT_HWD_LR) {
+            // R band of this tile: x' = q0 - dc - 63 + t, lane = d - dc, own pixel ql = lane + t - 63
+            const int nd = dce - dc;
+            for (int t = wave; t < 2 * CV_TX - 1; t += CV_WAVES) {
+                const int xr = q0 - dc - (CV_TX - 1) + t;
+                const int ql = lane + t - (CV_TX - 1);
+                if (xr >= 0 && xr < W && ql >= 0 && ql < CV_TX && lane < nd)
+                    out_r[((size_t)y * W + xr) * Dvol + dc + lane] = otile[ql * (CV_DC + 1) + lane];
             }
         }
     }
@@ -582,14 +598,22 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
         dim3 grid(cdiv(W, CV_TX), H);
         if (layout == SDE_LAYOUT_DHW) {
             cv64_kernel<SDE_SIDE_LEFT, OUT_DHW><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid, out_left,
-                                                                       nullptr, nullptr, nullptr);
+                                                                       nullptr, nullptr, nullptr, nullptr);
+        } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
+            // one pass: blocks past the row end (q < W + D - 1) only write R's invalid fill
+            const dim3 grid_lr(cdiv((int64_t)W + D - 1, CV_TX), H);
+            cv64_kernel<SDE_SIDE_LEFT, OUT_HWD_LR><<<grid_lr, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,
+                                                                              out_left, nullptr, nullptr, nullptr,
+                                                                              out_right);
         } else {
             if (sides & SDE_SIDE_LEFT)
                 cv64_kernel<SDE_SIDE_LEFT, OUT_HWD><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,
-                                                                           out_left, nullptr, nullptr, nullptr);
+                                                                           out_left, nullptr, nullptr, nullptr,
+                                                                           nullptr);
             if (sides & SDE_SIDE_RIGHT)
                 cv64_kernel<SDE_SIDE_RIGHT, OUT_HWD><<<grid, 256, 0, st>>>(fr, fl, H, W, 0, D, D, invalid,
-                                                                            out_right, nullptr, nullptr, nullptr);
+                                                                            out_right, nullptr, nullptr, nullptr,
+                                                                            nullptr);
         }
     } else {
         const int blocks = cdiv((int64_t)H * W, 256);
@@ -687,7 +711,7 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
     } else if (C == 64) {
         dim3 grid(cdiv(W, CV_TX), H);
         cv64_kernel<SDE_SIDE_LEFT, OUT_WTA><<<grid, 256, 0, st>>>(fl, fr, H, W, d0, d1, 0, -0.0f, nullptr,
-                                                                   min_cost, argmin, disp);
+                                                                   min_cost, argmin, disp, nullptr);
     } else {
         const int blocks = cdiv((int64_t)H * W, 256);
         cv_generic_kernel<OUT_WTA><<<blocks, 256, 0, st>>>(fl, fr, H, W, C, d0, d1, 0, SDE_SIDE_LEFT, -0.0f,

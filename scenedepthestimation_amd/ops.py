@@ -54,19 +54,24 @@ def _feat_pair(fl, fr):
 # cost volume / WTA (process_functional.py:48-131, 800-837)
 # ----------------------------------------------------------------------------
 def cost_volume(fl, fr, ndisp: int, layout: str = "DHW", right: bool = False, invalid=None,
-                out_left=None, out_right=None):
+                out_left=None, out_right=None, left: bool = True):
     """Exact cost volume.  DHW: compute_cost_volume (invalid -0.0).  HWD: GPU-path layout
-    with left and optionally right volumes (invalid 1.0, process_functional.py:1111)."""
+    with left and optionally right volumes (invalid 1.0, process_functional.py:1111); both
+    sides come from one pass (each voxel computed once, stored twice)."""
     pl, pr, H, W, C = _feat_pair(fl, fr)
     lay = LAYOUTS[layout]
     if invalid is None:
         invalid = -0.0 if layout == "DHW" else 1.0
     shape = (ndisp, H, W) if layout == "DHW" else (H, W, ndisp)
-    if out_left is None:
-        out_left = _empty(shape, torch.float32, fl)
-    ol = _need(out_left, "out_left", shape=shape)
-    orr = None
-    sides = SDE_SIDE_LEFT
+    if not left and not right:
+        raise ValueError("nothing to compute")
+    ol = orr = None
+    sides = 0
+    if left:
+        if out_left is None:
+            out_left = _empty(shape, torch.float32, fl)
+        ol = _need(out_left, "out_left", shape=shape)
+        sides |= SDE_SIDE_LEFT
     if right:
         if layout != "HWD":
             raise ValueError("the right volume exists in the HWD (GPU-path) layout only")
@@ -76,6 +81,8 @@ def cost_volume(fl, fr, ndisp: int, layout: str = "DHW", right: bool = False, in
         sides |= SDE_SIDE_RIGHT
     check(lib.sde_cost_volume(pl, pr, H, W, C, int(ndisp), lay, sides, ctypes.c_float(invalid), ol, orr,
                               _stream()), "sde_cost_volume")
+    if not left:
+        return out_right
     return (out_left, out_right) if right else out_left
 
 
