@@ -27,6 +27,7 @@ SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
 SDE_TOWER_FP32, SDE_TOWER_BF16X6 = 0, 1
 SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
 SDE_SGM_ACCUMULATE = 1
+SDE_SGM_ZERO_DU_PENALTIES = 2
 
 # name -> (restype, argtypes); must cover every function declared in include/sde.h
 SIGNATURES = {

@@ -174,7 +174,12 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
     }
 }
 
-template <int DPL, int PF, bool VEC, bool FIRST>
+// FIRST: S := f32(0 + L) (S is not read).  DU (direction UD only): also apply direction
+// DU in the same pass.  With the penalty channels 0/1 zero -- sgm_penelty_kernel never
+// writes them (:134-262) -- and finite costs, DU's recurrence collapses: b = m' exactly,
+// so L_DU = C at its first pixel (row H-1) and C + 0.0 elsewhere; the reference adds
+// it after UD (launch order :1166-1203), which per voxel is this same sequence.
+template <int DPL, int PF, bool VEC, bool FIRST, bool DU>
 __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
     const SgmSide sd = blockIdx.y ? s1 : s0;
@@ -233,6 +238,14 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
 #pragma unroll
             for (int i = 0; i < DPL; i++)
                 o[i] = FIRST ? (float)(0.0 + Ln[i]) : (float)((double)sl.s[i] + Ln[i]);
+            if (DU && k >= H - g.n) {          // UD visits row k; DU visits rows H-n .. H-1
+                const bool du_first = (k == H - 1);
+#pragma unroll
+                for (int i = 0; i < DPL; i++) {
+                    const double c = (double)sl.c[i];
+                    o[i] = (float)((double)o[i] + (du_first ? c : c + 0.0));
+                }
+            }
             if (k < g.n) {
                 if (VEC) {
                     if (dbase < D) {
@@ -259,54 +272,71 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             ahead.advance(g);
         }
     }
-    if (FIRST) {
-        // S := 0 + paths: pixels this direction never visits (UD stops at row n-1) start at 0
+    if (FIRST || DU) {
+        // rows UD never visits (it stops at row n-1): S := 0 (FIRST), then DU's term
         for (int r = g.n; r < H; r++) {
             const size_t off = ((size_t)r * W + line) * D;
 #pragma unroll
-            for (int i = 0; i < DPL; i++)
-                if (dbase + i < D) sd.S[off + dbase + i] = 0.0f;
+            for (int i = 0; i < DPL; i++) {
+                const int d = dbase + i;
+                if (d < D) {
+                    float v = FIRST ? 0.0f : sd.S[off + d];
+                    if (DU) {
+                        const double c = (double)sd.cv[off + d];
+                        v = (float)((double)v + (r == H - 1 ? c : c + 0.0));
+                    }
+                    sd.S[off + d] = v;
+                }
+            }
         }
     }
 }
 
-template <int DPL, bool VEC, bool FIRST>
+template <int DPL, bool VEC, bool FIRST, bool DU>
 static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
                         hipStream_t st)
 {
     const bool horiz = (dir == 2 || dir == 3);
     const int nlines = horiz ? H : W;
     constexpr int PF = DPL <= 4 ? 8 : 4;
-    sgm_scan_kernel<DPL, PF, VEC, FIRST><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
+    sgm_scan_kernel<DPL, PF, VEC, FIRST, DU><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
+}
+
+template <int DPL, bool VEC>
+static void launch_mode(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, bool first,
+                        bool du, hipStream_t st)
+{
+    if (first) {
+        if (du) launch_scan<DPL, VEC, true, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, VEC, true, false>(a, b, nsides, H, W, D, dir, st);
+    } else {
+        if (du) launch_scan<DPL, VEC, false, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, VEC, false, false>(a, b, nsides, H, W, D, dir, st);
+    }
 }
 
 template <int DPL>
 static void launch_dpl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, bool first,
-                       hipStream_t st)
+                       bool du, hipStream_t st)
 {
-    const bool vec = (D % DPL) == 0;
-    if (vec) {
-        if (first) launch_scan<DPL, true, true>(a, b, nsides, H, W, D, dir, st);
-        else launch_scan<DPL, true, false>(a, b, nsides, H, W, D, dir, st);
-    } else {
-        if (first) launch_scan<DPL, false, true>(a, b, nsides, H, W, D, dir, st);
-        else launch_scan<DPL, false, false>(a, b, nsides, H, W, D, dir, st);
-    }
+    if ((D % DPL) == 0) launch_mode<DPL, true>(a, b, nsides, H, W, D, dir, first, du, st);
+    else launch_mode<DPL, false>(a, b, nsides, H, W, D, dir, first, du, st);
 }
 
-// One direction over one or two sides; first: S := f32(0 + L) (no S read).
+// One direction over one or two sides; first: S := f32(0 + L) (no S read); du (dir 0
+// only): direction DU folded into the same pass (see sgm_scan_kernel).
 static int sgm_direction_impl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
-                              bool first, hipStream_t st)
+                              bool first, hipStream_t st, bool du = false)
 {
     switch ((D + 63) / 64) {
-    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, first, st); break;
-    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, first, st); break;
+    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, first, du, st); break;
     default: return SDE_ERR_ARG;
     }
     return SDE_OK;
@@ -534,15 +564,19 @@ SDE_EXPORT int sde_sgm_8path(const float *cv, const float *pen, int H, int W, in
 SDE_EXPORT int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r,
                                   const float *pen_r, float *S_r, int H, int W, int D, int flags, void *stream)
 {
-    if (!cv_l || !pen_l || !S_l || H < 2 || W < 2 || D <= 0 || D > 512 || (flags & ~SDE_SGM_ACCUMULATE))
+    if (!cv_l || !pen_l || !S_l || H < 2 || W < 2 || D <= 0 || D > 512 ||
+        (flags & ~(SDE_SGM_ACCUMULATE | SDE_SGM_ZERO_DU_PENALTIES)))
         return SDE_ERR_ARG;
     const bool two = cv_r || pen_r || S_r;
     if (two && (!cv_r || !pen_r || !S_r)) return SDE_ERR_ARG;
     const SgmSide a{cv_l, pen_l, S_l};
     const SgmSide b = two ? SgmSide{cv_r, pen_r, S_r} : a;
+    const bool fold_du = (flags & SDE_SGM_ZERO_DU_PENALTIES) != 0;
     for (int dir = 0; dir < 8; dir++) {
+        if (dir == 1 && fold_du) continue;                               // applied in the UD pass
         const bool first = dir == 0 && !(flags & SDE_SGM_ACCUMULATE);   // UD: line = column
-        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, as_stream(stream));
+        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, as_stream(stream),
+                                         dir == 0 && fold_du);
         if (s != SDE_OK) return s;
     }
     return launch_status();

@@ -328,10 +328,12 @@ def sgm_8path(cv_hwd, pen, S=None):
     return S
 
 
-def sgm_8path_pair(cv_l, pen_l, S_l, cv_r=None, pen_r=None, S_r=None, accumulate=False):
+def sgm_8path_pair(cv_l, pen_l, S_l, cv_r=None, pen_r=None, S_r=None, accumulate=False, zero_du_penalties=False):
     """8-path SGM of both image sides, one launch per direction (sde_sgm_8path_pair).
 
-    accumulate=False: S := the 8-path sum from zero (S need not be zeroed)."""
+    accumulate=False: S := the 8-path sum from zero (S need not be zeroed).
+    zero_du_penalties=True: the penalties come from sgm_penalties (channels 0/1 zero) and
+    the costs are finite -- direction DU is folded into the UD pass (same values)."""
     H, W, D = cv_l.shape
     args = [_need(cv_l, "cost volume"), _need(pen_l, "penalties", shape=(H, W, 16)), _need(S_l, "S", shape=(H, W, D))]
     if cv_r is None:
@@ -339,8 +341,9 @@ def sgm_8path_pair(cv_l, pen_l, S_l, cv_r=None, pen_r=None, S_r=None, accumulate
     else:
         args += [_need(cv_r, "cost volume", shape=(H, W, D)), _need(pen_r, "penalties", shape=(H, W, 16)),
                  _need(S_r, "S", shape=(H, W, D))]
-    check(lib.sde_sgm_8path_pair(*args, H, W, D, _lib.SDE_SGM_ACCUMULATE if accumulate else 0, _stream()),
-          "sde_sgm_8path_pair")
+    flags = (_lib.SDE_SGM_ACCUMULATE if accumulate else 0) | \
+        (_lib.SDE_SGM_ZERO_DU_PENALTIES if zero_du_penalties else 0)
+    check(lib.sde_sgm_8path_pair(*args, H, W, D, flags, _stream()), "sde_sgm_8path_pair")
     return S_l, S_r
 
 
