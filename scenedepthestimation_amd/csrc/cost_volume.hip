@@ -276,8 +276,9 @@ __global__ __launch_bounds__(256) void argmin_merge_kernel(const float *__restri
 // fp32.  Rigorous bound for every voxel of a pixel (Cauchy-Schwarz on |a|,|b|):
 //   |s_fast - s_true| <= (3*2^-16 + 192*2^-23) * sum|a_c b_c|   (split + accumulation)
 //   |s_exact - s_true| <= 10*2^-24 * sum|a_c b_c|               (NumPy pairwise order)
-//   => |s_fast - s_exact| <= FX_K * sum|a_c b_c| <= FX_K * ||fl[x]||_1 * max_window |fr|
-//      (FX_K = 1e-4: 1.4x margin over 7e-5)
+//   => |s_fast - s_exact| <= FX_K * sum|a_c b_c| <= FX_K * ||fl[x]||_2 * max_window ||fr||_2
+//      (FX_K = 1e-4: 1.4x margin over 7e-5; the per-pixel L2 norms are fp32 sums of
+//      squares inflated by 1 + 4e-6, an upper bound)
 // If the best fast score beats the runner-up by more than 2 eps, the exact
 // first-min is provably the fast argmax (no other d can tie or win exactly),
 // and its exact cost is computed once (same arithmetic as cv64_kernel).  Any
@@ -287,10 +288,12 @@ __global__ __launch_bounds__(256) void argmin_merge_kernel(const float *__restri
 //
 // Mapping: workgroup = 4 waves on one row and 64 left pixels (2 N-tiles of 32);
 // the right-feature window of a <=128-disparity chunk (<= 6 M-tiles of 32
-// pixels) is split once into hi/lo bf16 planes in LDS (16-B XOR swizzle by
-// pixel>>1); wave w owns N-tile w&1 and every other M-tile; the left operand
-// lives in registers (hi/lo, 32 VGPRs).  Blocks are remapped so all blocks of
-// a row run on one XCD (its L2 serves the overlapping windows).
+// pixels) arrives pre-split as hi/lo bf16 planes (written by the tower's last
+// epilogue or feature_split_kernel) and is staged into LDS by LDS-DMA
+// (global_load_lds, swizzle applied to the source address); wave w owns N-tile
+// w&1 and every other M-tile; the left operand lives in registers (hi/lo).
+// Blocks are remapped so all blocks of a row run on one XCD (its L2 serves the
+// overlapping windows).
 // ===========================================================================
 typedef __bf16 fx_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float fx_floatx16 __attribute__((ext_vector_type(16)));
