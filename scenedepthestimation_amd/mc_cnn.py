@@ -4,8 +4,9 @@ The reference builds `Net` (mc_cnn_brunch.py:4-67) with variables named
 ``conv{k}/weights:0`` (HWIO ``[3,3,Cin,nf]``) and ``conv{k}/biases:0`` (``[nf]``)
 (`conv`, mc_cnn_brunch.py:70-92) and restores them from a TF1 checkpoint
 (process_functional.py:24-33) or a ``.npy`` dict (`load_initial_weights`,
-mc_cnn_brunch.py:51-58).  No checkpoint ships with the reference, so the
-default here is a seeded synthetic He-normal initialisation of the same
+mc_cnn_brunch.py:51-58).  TF1 checkpoints are read without TensorFlow by
+``tf_checkpoint.load_checkpoint``.  No checkpoint ships with the reference, so
+the default here is a seeded synthetic He-normal initialisation of the same
 architecture.  The device-side network is run by ``ops.tower_forward``.
 """
 from __future__ import annotations
@@ -39,10 +40,12 @@ def load_weights(checkpoint, nlayers: int, allow_pickle: bool = False) -> dict:
     """Load a weights dict keyed like the reference's trainable variables.
 
     Accepted: a dict; ``synthetic`` / ``synthetic:<seed>`` / None; a ``.npz`` or
-    ``.safetensors`` file with the reference variable names; a ``.npy`` dict as
-    written by ``Net.save_weights_dict`` (pickled, so only with allow_pickle=True
-    for a file the caller trusts).  A TF1 checkpoint prefix (``*.ckpt``) is not
-    readable without TensorFlow: FileNotFoundError / ValueError like TF's restore.
+    ``.safetensors`` file with the reference variable names; a TF1 (Saver V2)
+    checkpoint prefix such as ``model_epoch14.ckpt`` (``<prefix>.index`` +
+    ``<prefix>.data-*``, read by tf_checkpoint.py); a ``.npy`` dict as written by
+    ``Net.save_weights_dict`` (pickled, so only with allow_pickle=True for a file
+    the caller trusts).  A missing checkpoint raises FileNotFoundError, like TF's
+    restore.
     """
     if checkpoint is None:
         return synthetic_weights(nlayers)
@@ -65,10 +68,9 @@ def load_weights(checkpoint, nlayers: int, allow_pickle: bool = False) -> dict:
                                  "file you trust, or convert it to .npz / .safetensors")
             w = np.load(path, allow_pickle=True, encoding="bytes").item()
         else:
-            if not os.path.exists(path) and not os.path.exists(path + ".index"):
-                raise FileNotFoundError(f"checkpoint {path!r} not found")
-            raise ValueError(f"{path!r}: TF1 checkpoints need TensorFlow to read; export the variables "
-                             "conv{k}/weights:0, conv{k}/biases:0 to .npz")
+            from . import tf_checkpoint
+            names = [n for pair in var_names(nlayers) for n in pair]
+            w = {n: v for n, v in zip(names, tf_checkpoint.load_checkpoint(path, names).values())}
     w = {(k.decode() if isinstance(k, bytes) else k): np.asarray(v, dtype=np.float32) for k, v in w.items()}
     for wn, bn in var_names(nlayers):
         if wn not in w or bn not in w:
