@@ -113,7 +113,10 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     def tower(i, timed):
         e_t = t_tower.start() if timed else None
         ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
-        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i], precision=m.tower_precision)
+        # bf16x6: intermediate activations in the c-block-major layout, as sde_tower_forward runs them
+        cbl = m.tower_precision == "bf16x6"
+        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i], precision=m.tower_precision,
+                        out_cblock=cbl and L > 2)
         hin, win = H + 2 * L - 4, W + 2 * L - 4
         cur = 0
         for layer in range(3, L + 1):
@@ -124,7 +127,8 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
             src = acts[cur].view(-1)[: hin * win * NF].view(hin, win, NF)
             e = t_conv.start() if (timed and layer == 3) else None
             ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision,
-                            split=m.split[i] if (layer == L and m.split) else None)
+                            split=m.split[i] if (layer == L and m.split) else None,
+                            in_cblock=cbl, out_cblock=cbl and layer < L)
             if e is not None:
                 t_conv.stop(e)
             hin, win = hin - 2, win - 2
@@ -341,7 +345,7 @@ def main():
             if m.tower_precision == "bf16x6":
                 # six bf16 partial products per fp32 product: the roof is the dense bf16 MFMA rate
                 ach = 6 * fl / (conv_ms * 1e-3) / 1e12
-                roof = {"kernel": "conv64_x6_kernel<false,false> (tower layer 3, bf16x6)", "bound": "mfma",
+                roof = {"kernel": "conv64_x6p_kernel<false,false,true,true> (tower layer 3, bf16x6)", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,
                         "traffic": None,
                         "per_launch": f"6 x {fl / 1e9:.2f} GFLOP bf16 (2*{hout}*{wout}*64*576 fp32-equivalent) "

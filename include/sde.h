@@ -138,6 +138,11 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
 #define SDE_TOWER_FP32 0      /* v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation            */
 #define SDE_TOWER_BF16X6 1    /* fp32 operands split exactly into 3 bf16 parts, the 6 leading partial products
                                  on v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level error, 2.67x rate */
+/* sde_tower_layer only, with SDE_TOWER_BF16X6: intermediate activations in the c-block-major
+ * layout [nf/16][h][w][16] that sde_tower_forward uses between layers (16-channel blocks
+ * contiguous per pixel run).  IN: `in` of a layer >= 3; OUT: `out` of a layer < nlayers. */
+#define SDE_TOWER_IN_CBLOCK 2
+#define SDE_TOWER_OUT_CBLOCK 4
 
 /* Number of floats of the packed (device-layout) weight blob (fp32 + pre-split bf16 planes). */
 int64_t sde_tower_packed_floats(int nlayers, int nf);

@@ -1,25 +1,23 @@
-// tower.hip -- MC-CNN-fast Siamese branch on fp32 MFMA (gfx950).
+// tower.hip -- MC-CNN-fast Siamese branch on the MFMA units (gfx950).
 //
 // Replaces mc_cnn_brunch.py:31-48 (Net.construct) + :70-92 (conv) as run by
 // compute_feature (process_functional.py:21-39): nlayers x [3x3 VALID conv,
 // bias, ReLU] (no ReLU on the last), then tf.nn.l2_normalize over channels.
+// Layers 2..n are implicit GEMMs: out[n][pixel] = sum over (tap, c) of
+// W[tap][n][c] * in[pixel + tap][c], M = 64 output maps, K = 9 taps x 64 maps.
+// Layer 1 (Cin = 1, 9 MACs per output) is computed on VALU straight into layer
+// 2's input staging, so its output never touches HBM; the last layer's epilogue
+// L2-normalises each pixel (and can emit the certified cost volume's bf16 split
+// planes and norm bounds).
 //
-// Layers 2..n are an implicit GEMM on v_mfma_f32_32x32x2_f32 (exact f32 in /
-// f32 accumulate, the 157 TF fp32 matrix rate): out[n][pixel] = sum over
-// (tap, c) of W[tap][n][c] * in[pixel + tap][c].  A = weights (M = 64 output
-// maps = 2 tiles of 32), B = input pixels (N = 32 pixels of one output row),
-// K = 64 input maps per tap x 9 taps.
-//
-// Workgroup: 512 threads = 8 waves, output tile 8 rows x 32 columns, wave w
-// owns output row w (2 accumulators of 32x32).  LDS: the (8+2) x (32+2) x 64
-// input tile (87 KB) stays resident for all 9 taps; each tap's 64x64 weight
-// slice (16 KB) is double-buffered (prefetched into registers during the
-// previous tap's MFMAs).  Both LDS images are XOR-swizzled at 8-B granularity
-// (pair slot ^= row & 31) so the 32 lanes of a ds_read_b64 half hit 64
-// distinct banks.  Layer 1 (Cin = 1, 9 MACs per output) is computed on VALU
-// straight into layer 2's LDS input tile, so its output never touches HBM; the
-// last layer's epilogue L2-normalises each pixel (its 64 channels live in a
-// lane pair l, l^32) before the store.
+// Two arithmetics (SDE_TOWER_FP32 / SDE_TOWER_BF16X6):
+// * conv64_mfma_kernel: v_mfma_f32_32x32x2_f32 (exact f32 products, the 157 TF
+//   fp32 matrix rate).  512 threads, output tile 8 rows x 32 columns, wave w owns
+//   output row w (2 accumulators of 32x32); the (8+2) x (32+2) x 64 input tile
+//   (87 KB) stays in LDS for all 9 taps, each tap's 64x64 weight slice is
+//   double-buffered; both LDS images XOR-swizzled at 8-B granularity.
+// * conv64_x6p_kernel (default): fp32 operands split exactly into three bf16
+//   parts, six partial products on v_mfma_f32_32x32x16_bf16 -- see below.
 #include "sde_common.h"
 
 #include <algorithm>
@@ -37,7 +35,8 @@ constexpr int TW_NPIX = TW_IY * TW_IX;   // 340
 constexpr int NF = 64;                   // feature maps (the reference's num_of_conv_feature_maps)
 constexpr int L1_FLOATS = NF + 9 * NF;           // bias + [tap][n]
 constexpr int LK_W = 9 * NF * NF;                // one [tap][n][c] plane, elements
-// layer k >= 2: bias f32 [64] | W f32 [tap][n][c] | 3 bf16 planes [p][tap][n][c] (hi, mid, lo: W = hi+mid+lo)
+// layer k >= 2: bias f32 [64] | W f32 [tap][n][c] | bf16 parts (hi, mid, lo: W = hi+mid+lo) in A-fragment order
+// [mtile 2][cblock 4][tap 9][part 3][lane 64][8] for conv64_x6p_kernel
 constexpr int LK_FLOATS = NF + LK_W + 3 * LK_W / 2;
 
 // float2 slot of channel pair `pair` (0..31) of pixel/row `p` in a swizzled 64-float row
@@ -240,12 +239,29 @@ __global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restric
 // (RNE; each residual is exact in f32), and the six partial products with
 // i + j <= 2 are accumulated in fp32 (the three dropped ones are < 2^-23 |ab|,
 // below one fp32 rounding of the product).  16x the fp32 MFMA rate / 6 terms =
-// 2.67x the fp32 matrix peak at fp32-level error.  Weights arrive pre-split
-// (host packing); activations are split in registers from the fp32 LDS tile.
-// Same tiling as conv64_mfma_kernel; LDS: fp32 tile (16-B XOR swizzle by pixel)
-// + double-buffered 3 x [64 n][64 c] bf16 weight planes (16-B swizzle by n>>1).
+// 2.67x the fp32 matrix peak at fp32-level error.
+//
+// conv64_x6p_kernel: persistent, one 512-thread workgroup per CU walking 16 x 32
+// output tiles, warp-specialised:
+// * waves 0-3 (one per SIMD) only issue MFMAs.  Wave w owns output channels
+//   32*(w&1)..+31 and output rows 8*(w>>1)..+7 of the tile: 8 accumulators,
+//   48 MFMAs per tap.  Weights never touch LDS: they are pre-arranged on the
+//   host in A-fragment order [mtile][cblock][tap][part][lane][8] and read
+//   straight into VGPRs one tap ahead (L2-resident, 221 KB per layer).
+// * waves 4-7 (the "stagers") stream the input: the contraction is cut into
+//   16-channel blocks (c-blocks); for one c-block the 18 x 34 input pixels are
+//   loaded, split ONCE into bf16 parts and written to LDS as six planes (3 parts
+//   x 2 channel halves, 8 bf16 per pixel) so that a B fragment is one contiguous,
+//   conflict-free 1-KB ds_read_b128.  Two stage buffers: the stagers fill c-block
+//   k+1 (or the next tile's first) while the MFMA waves consume c-block k; one
+//   workgroup barrier per c-block.  Keeping the long-latency HBM loads in other
+//   waves keeps them out of the MFMA waves' in-order vmcnt.
+// Inter-layer activations use a c-block-major layout [4][h][w][16] (IN_CB /
+// OUT_CB) so a stage reads contiguous 64-B pixel runs; the last layer writes the
+// reference's [h][w][64].
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
 {
@@ -256,178 +272,330 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
     l = (__bf16)r2;
 }
 
-// tile image: pixel p, 16-B chunk q (channels 4q..4q+3)
-__device__ __forceinline__ int tslot(int p, int q) { return p * 16 + (q ^ (p & 15)); }
-// weight plane image: row n, 16-B chunk c8 (channels 8c8..8c8+7)
-__device__ __forceinline__ int wslot(int n, int c8) { return n * 8 + (c8 ^ ((n >> 1) & 7)); }
+constexpr int XP_TY = 16, XP_TX = 32;             // output tile
+constexpr int XP_IY = XP_TY + 2, XP_IX = XP_TX + 2;
+constexpr int XP_NPIX = XP_IY * XP_IX;            // 612 input pixels per tile
+constexpr int XP_PLANE = XP_NPIX * 16;            // bytes of one (part, channel-half) plane
+constexpr int XP_STAGE = 6 * XP_PLANE;            // one c-block stage: 58,752 B
+constexpr int XP_UNITS = XP_NPIX * 4;             // (pixel, 4-channel chunk) units per stage
+constexpr int XP_STAGERS = 256;                   // threads of the stager waves
+constexpr int XP_UPT = (XP_UNITS + XP_STAGERS - 1) / XP_STAGERS;   // units per stager thread (10)
+constexpr int XP_ROWS = 8;                        // output rows per MFMA wave
+constexpr int XP_RED = 2 * 2 * XP_TY * XP_TX * 4; // LAST: two per-M-tile partial-sum exchanges
+constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + XP_RED;
+constexpr int XP_NCB = NF / 16;                   // c-blocks per pixel
 
-constexpr int X6_TILE_BYTES = TW_NPIX * NF * 4;             // 87,040
-constexpr int X6_WBUF_BYTES = 3 * NF * NF * 2;              // 24,576 per tap buffer
-constexpr size_t X6_SMEM = (size_t)X6_TILE_BYTES + 2 * X6_WBUF_BYTES;
-
-template <bool FIRST, bool LAST>
-__global__ __launch_bounds__(512) void conv64_x6_kernel(const float *__restrict__ in, int Hin, int Win,
-                                                        const float *__restrict__ w1blob,
-                                                        const float *__restrict__ wkblob,
-                                                        float *__restrict__ out, int Hout, int Wout,
-                                                        uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
-                                                        float *__restrict__ onrm)
+// Split 4 channels and store them into the stage's six planes.
+__device__ __forceinline__ void xp_put(char *sb, int u, float4 v)
 {
-    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
-    float4 *tile = smem4;                                                    // [340][16] float4
-    uint4 *wbuf0 = reinterpret_cast<uint4 *>(smem4 + X6_TILE_BYTES / 16);    // [3][64][8] uint4
-    uint4 *wbuf1 = wbuf0 + X6_WBUF_BYTES / 16;
+    const int px = u >> 2, chunk = u & 3;
+    bf16x4 p0, p1, p2;
+    const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        __bf16 a, b, c;
+        split3(xs[e], a, b, c);
+        p0[e] = a; p1[e] = b; p2[e] = c;
+    }
+    char *dst = sb + (chunk >> 1) * XP_PLANE + px * 16 + (chunk & 1) * 8;
+    *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
+    *reinterpret_cast<uint2 *>(dst + 2 * XP_PLANE) = __builtin_bit_cast(uint2, p1);
+    *reinterpret_cast<uint2 *>(dst + 4 * XP_PLANE) = __builtin_bit_cast(uint2, p2);
+}
+
+// One stage unit of activations (zero outside the input).
+template <bool IN_CB>
+__device__ __forceinline__ float4 xp_load(const float *__restrict__ in, int Hin, int Win, int ty0, int tx0, int cb,
+                                          int u)
+{
+    const int px = u >> 2, chunk = u & 3;
+    const int iy = px / XP_IX, ix = px - iy * XP_IX;
+    const int y = ty0 + iy, x = tx0 + ix;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y < Hin && x < Win) {
+        const float4 *in4 = reinterpret_cast<const float4 *>(in);
+        v = IN_CB ? in4[(((size_t)cb * Hin + y) * Win + x) * 4 + chunk] : in4[((size_t)y * Win + x) * 16 + cb * 4 + chunk];
+    }
+    return v;
+}
+
+// conv1 (Cin = 1, 3x3, bias, ReLU) of the padded image for one stage unit; w = the 9 taps x
+// 4 channels of the unit's chunk, b = their biases (a stager thread's chunk is fixed).
+__device__ __forceinline__ float4 xp_conv1(const float *__restrict__ img, int Hin, int Win, const float4 (&w)[9],
+                                           float4 b, int ty0, int tx0, int u)
+{
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int px = u >> 2;
+    const int iy = px / XP_IX, ix = px - iy * XP_IX;
+    const int y = ty0 + iy, x = tx0 + ix;
+    if (y < Hin - 2 && x < Win - 2) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            const float im = img[(size_t)(y + t / 3) * Win + x + t % 3];
+            s0 = fmaf(im, w[t].x, s0);
+            s1 = fmaf(im, w[t].y, s1);
+            s2 = fmaf(im, w[t].z, s2);
+            s3 = fmaf(im, w[t].w, s3);
+        }
+        v = make_float4(fmaxf(s0 + b.x, 0.f), fmaxf(s1 + b.y, 0.f), fmaxf(s2 + b.z, 0.f), fmaxf(s3 + b.w, 0.f));
+    }
+    return v;
+}
+
+// Stager waves: fill one stage with c-block cb of tile t.
+template <bool FIRST, bool IN_CB>
+__device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, int Hin, int Win,
+                                        const float *__restrict__ w1blob, int t, int tiles_x, int cb, int st)
+{
+    // opaque to the optimiser: stops loop-invariant code motion from hoisting the per-unit
+    // address arithmetic of all units out of the tile loop (it would pin ~40 VGPRs that the
+    // MFMA waves' accumulators need)
+    asm volatile("" : "+v"(st));
+    const int ty0 = (t / tiles_x) * XP_TY, tx0 = (t % tiles_x) * XP_TX;
+    if (FIRST) {
+        // the thread's chunk is st & 3 for every unit (XP_STAGERS is a multiple of 4)
+        const int n0 = cb * 16 + (st & 3) * 4;
+        const float4 b = *reinterpret_cast<const float4 *>(w1blob + n0);
+        float4 w[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) w[t] = *reinterpret_cast<const float4 *>(w1blob + NF + t * NF + n0);
+#pragma unroll 2
+        for (int i = 0; i < XP_UPT; i++) {
+            const int u = st + i * XP_STAGERS;
+            if (u < XP_UNITS) xp_put(sb, u, xp_conv1(in, Hin, Win, w, b, ty0, tx0, u));
+        }
+    } else {
+        // two batches of 5 loads in flight (the stagers have time; registers are shared
+        // with the MFMA waves' allocation)
+        constexpr int HB = (XP_UPT + 1) / 2;
+#pragma unroll
+        for (int b0 = 0; b0 < XP_UPT; b0 += HB) {
+            float4 v[HB];
+#pragma unroll
+            for (int i = 0; i < HB; i++) {
+                const int u = st + (b0 + i) * XP_STAGERS;
+                v[i] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < HB; i++) {
+                const int u = st + (b0 + i) * XP_STAGERS;
+                if (u < XP_UNITS) xp_put(sb, u, v[i]);
+            }
+        }
+    }
+}
+
+struct XpFrag {
+    bf16x8 p[3];
+};
+
+__device__ __forceinline__ XpFrag xp_afrag(const uint4 *__restrict__ wf, int mt, int cb, int tap, int lane)
+{
+    const uint4 *src = wf + ((size_t)((mt * XP_NCB + cb) * 9 + tap) * 3) * 64 + lane;
+    XpFrag f;
+#pragma unroll
+    for (int q = 0; q < 3; q++) f.p[q] = __builtin_bit_cast(bf16x8, src[q * 64]);
+    return f;
+}
+
+// B fragments (three parts) of one row-step.
+struct XpB {
+    bf16x8 p[3];
+};
+
+__device__ __forceinline__ XpB xp_bfrag(const char *b)
+{
+    XpB f;
+#pragma unroll
+    for (int q = 0; q < 3; q++) f.p[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(b + 2 * q * XP_PLANE));
+    return f;
+}
+
+// One c-block for one MFMA wave: 9 taps x 8 rows = 72 row-steps of 6 MFMAs (small terms
+// first, the leading product last).  B fragments are read two row-steps ahead (a 3-deep
+// register ring) and sched_barrier fences keep the scheduler from hoisting more, which
+// bounds the live registers (8 accumulators = 128 of the 256 a wave may hold at 2 waves
+// per SIMD).  A fragments for tap t+1 are requested when tap t starts.  Rows past the
+// output edge run on zero-filled input and are discarded by the epilogue.
+__device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ROWS], XpFrag (&an)[2], const uint4 *__restrict__ wf,
+                                          int mt, int cb, int ncb, int lane, const char *sb)
+{
+    constexpr int NS = 9 * XP_ROWS;
+    XpB ring[3];
+    auto boff = [&](int s) { return ((s / XP_ROWS / 3 + s % XP_ROWS) * XP_IX + (s / XP_ROWS) % 3) * 16; };
+    ring[0] = xp_bfrag(sb + boff(0));
+    ring[1] = xp_bfrag(sb + boff(1));
+    XpFrag a = an[0];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int tap = s / XP_ROWS, r = s % XP_ROWS;
+        if (r == 0) {
+            // A fragments two taps ahead: an[0] = A(tap + 1), an[1] = A(tap + 2)
+            if (tap > 0) a = an[0];
+            an[0] = an[1];
+            an[1] = tap < 7 ? xp_afrag(wf, mt, cb, tap + 2, lane) : xp_afrag(wf, mt, ncb, tap - 7, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const XpB &b = ring[s % 3];
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc[r], 0, 0, 0);
+        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc[r], 0, 0, 0);
+        if (s + 2 < NS) ring[(s + 2) % 3] = xp_bfrag(sb + boff(s + 2));
+    }
+}
+
+template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB>
+__global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict__ in, int Hin, int Win,
+                                                         const float *__restrict__ w1blob,
+                                                         const float *__restrict__ wkblob,
+                                                         float *__restrict__ out, int Hout, int Wout,
+                                                         uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
+                                                         float *__restrict__ onrm, int tiles_x, int ntiles)
+{
+    extern __shared__ __attribute__((aligned(16))) char xsm[];
+    float *red0 = reinterpret_cast<float *>(xsm + 2 * XP_STAGE);   // [2 mt][16 rows][32 px]
+    float *red1 = red0 + 2 * XP_TY * XP_TX;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int tx0 = blockIdx.x * TW_TX;
-    const int ty0 = blockIdx.y * TW_TY;
+    const bool mfma_wave = wave < 4;            // waves 4..7 stage the input
+    const int mt = wave & 1, g = (wave >> 1) & 1;
+    const int st = tid - XP_STAGERS;            // stager thread index (valid when !mfma_wave)
     const float *bias = wkblob;
-    const uint4 *planes = reinterpret_cast<const uint4 *>(wkblob + NF + LK_W);   // [3][9][64][8] uint4
+    const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + NF + LK_W);
+    // B fragment: plane (part, h), input row 8g + r + ky, pixel j + kx
+    const int bbase = (lane >> 5) * XP_PLANE + ((XP_ROWS * g) * XP_IX + (lane & 31)) * 16;
 
-    // weight prefetch: thread t moves chunk (n = t>>3, c8 = t&7) of each plane
-    const int wn = tid >> 3, wc8 = tid & 7;
-    const size_t wofs = (size_t)wn * 8 + wc8;
-    constexpr size_t PSTRIDE = (size_t)9 * NF * 8;      // uint4 per plane
-    uint4 wr0 = planes[wofs], wr1 = planes[PSTRIDE + wofs], wr2 = planes[2 * PSTRIDE + wofs];
-
-    if (!FIRST) {
-        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
-            const int p = idx >> 4, q = idx & 15;
-            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (iy < Hin && ix < Win) v = reinterpret_cast<const float4 *>(in + ((size_t)iy * Win + ix) * NF)[q];
-            tile[tslot(p, q)] = v;
-        }
-    } else {
-        const float *b1 = w1blob;
-        const float *w1 = w1blob + NF;
-        const int H1 = Hin - 2, W1 = Win - 2;
-        for (int idx = tid; idx < TW_NPIX * 16; idx += 512) {
-            const int p = idx >> 4, q = idx & 15;
-            const int iy = ty0 + p / TW_IX, ix = tx0 + p % TW_IX;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (iy < H1 && ix < W1) {
-                float im[9];
-#pragma unroll
-                for (int t = 0; t < 9; t++) im[t] = in[(size_t)(iy + t / 3) * Win + ix + t % 3];
-                float a[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int n = 4 * q + j;
-                    float s = 0.0f;
-#pragma unroll
-                    for (int t = 0; t < 9; t++) s = fmaf(im[t], w1[t * NF + n], s);
-                    s += b1[n];
-                    a[j] = s > 0.0f ? s : 0.0f;
-                }
-                v = make_float4(a[0], a[1], a[2], a[3]);
-            }
-            tile[tslot(p, q)] = v;
-        }
+    int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    XpFrag an[2];
+    if (mfma_wave) {
+        an[0] = xp_afrag(wf, mt, 0, 0, lane);
+        an[1] = xp_afrag(wf, mt, 0, 1, lane);
     }
-    {
-        const int ws = wslot(wn, wc8);
-        wbuf0[ws] = wr0;
-        wbuf0[NF * 8 + ws] = wr1;
-        wbuf0[2 * NF * 8 + ws] = wr2;
-    }
+    else xp_fill<FIRST, IN_CB>(xsm, in, Hin, Win, w1blob, tile, tiles_x, 0, st);
     __syncthreads();
 
-    floatx16 acc0 = {0}, acc1 = {0};
-    const int j = lane & 31;
-    const int h = lane >> 5;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; tap++) {
-        const int ky = tap / 3, kx = tap - 3 * ky;
-        const uint4 *wb = (tap & 1) ? wbuf1 : wbuf0;
-        if (tap < 8) {
-            const size_t o = (size_t)(tap + 1) * NF * 8 + wofs;
-            wr0 = planes[o];
-            wr1 = planes[PSTRIDE + o];
-            wr2 = planes[2 * PSTRIDE + o];
-        }
-        const int p = (wave + ky) * TW_IX + (j + kx);
+    int cur = 0;
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int ty0 = (tile / tiles_x) * XP_TY, tx0 = (tile % tiles_x) * XP_TX;
+        floatx16 acc[XP_ROWS];
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const float4 x0 = tile[tslot(p, 4 * s + 2 * h)];
-            const float4 x1 = tile[tslot(p, 4 * s + 2 * h + 1)];
-            const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            bf16x8 b0, b1, b2;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                __bf16 hh, mm, ll;
-                split3(xv[i], hh, mm, ll);
-                b0[i] = hh; b1[i] = mm; b2[i] = ll;
-            }
-            const int c8 = 2 * s + h;
-            const int s0 = wslot(j, c8), s1 = wslot(32 + j, c8);
-            const bf16x8 a00 = __builtin_bit_cast(bf16x8, wb[s0]);
-            const bf16x8 a01 = __builtin_bit_cast(bf16x8, wb[NF * 8 + s0]);
-            const bf16x8 a02 = __builtin_bit_cast(bf16x8, wb[2 * NF * 8 + s0]);
-            const bf16x8 a10 = __builtin_bit_cast(bf16x8, wb[s1]);
-            const bf16x8 a11 = __builtin_bit_cast(bf16x8, wb[NF * 8 + s1]);
-            const bf16x8 a12 = __builtin_bit_cast(bf16x8, wb[2 * NF * 8 + s1]);
-            // small terms first, the leading product last
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a02, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a12, b0, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a01, b1, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a11, b1, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b2, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b2, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a01, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a11, b0, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b1, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b1, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a00, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a10, b0, acc1, 0, 0, 0);
-        }
-        if (tap < 8) {
-            uint4 *nb = (tap & 1) ? wbuf0 : wbuf1;
-            const int ws = wslot(wn, wc8);
-            nb[ws] = wr0;
-            nb[NF * 8 + ws] = wr1;
-            nb[2 * NF * 8 + ws] = wr2;
-        }
-        __syncthreads();
-    }
+        for (int r = 0; r < XP_ROWS; r++) acc[r] = floatx16{0};
 
-    float v[2][16];
+#pragma unroll 1
+        for (int cb = 0; cb < XP_NCB; cb++) {
+            const int ntile = cb + 1 < XP_NCB ? tile : tile + (int)gridDim.x;
+            const int ncb = (cb + 1) & (XP_NCB - 1);
+            if (mfma_wave) {
+                xp_cblock(acc, an, wf, mt, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
+            } else if (ntile < ntiles) {
+                xp_fill<FIRST, IN_CB>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, tiles_x, ncb, st);
+            }
+            if (cb == XP_NCB - 1) {
+                // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
+                // lane holds pixel column j, channels mt*32 + 8q + 4h + e in acc[r][4q + e]
+                // opaque copies of the lane coordinates: keep the epilogue's bias loads and
+                // addresses inside the loop (hoisted, they would pin registers for the whole kernel)
+                int j = lane & 31, h = lane >> 5;
+                asm volatile("" : "+v"(j), "+v"(h));
+                float bv[16];
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const int n = 8 * (r >> 2) + 4 * h + (r & 3);
-        v[0][r] = acc0[r] + bias[n];
-        v[1][r] = acc1[r] + bias[32 + n];
-    }
-    if (!LAST) {
+                for (int i = 0; i < 16; i++) bv[i] = bias[mt * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+                if (!LAST) {
+                    if (mfma_wave) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-            v[0][r] = v[0][r] > 0.0f ? v[0][r] : 0.0f;
-            v[1][r] = v[1][r] > 0.0f ? v[1][r] : 0.0f;
+                        for (int r = 0; r < XP_ROWS; r++) {
+                            const int y = ty0 + XP_ROWS * g + r, x = tx0 + j;
+                            if (y < Hout && x < Wout) {
+#pragma unroll
+                                for (int q = 0; q < 4; q++) {
+                                    const float4 o = make_float4(fmaxf(acc[r][4 * q] + bv[4 * q], 0.f),
+                                                                 fmaxf(acc[r][4 * q + 1] + bv[4 * q + 1], 0.f),
+                                                                 fmaxf(acc[r][4 * q + 2] + bv[4 * q + 2], 0.f),
+                                                                 fmaxf(acc[r][4 * q + 3] + bv[4 * q + 3], 0.f));
+                                    const int c = mt * 32 + 8 * q + 4 * h;
+                                    float *dst = OUT_CB ? out + (((size_t)(c >> 4) * Hout + y) * Wout + x) * 16 + (c & 15)
+                                                        : out + ((size_t)y * Wout + x) * NF + c;
+                                    *reinterpret_cast<float4 *>(dst) = o;
+                                }
+                            }
+                        }
+                    }
+                } else {
+                    // a pixel's 64 channels live in two waves (mt = 0, 1): the sums of
+                    // squares are exchanged through LDS (every wave joins the barriers)
+                    if (mfma_wave) {
+#pragma unroll
+                        for (int r = 0; r < XP_ROWS; r++) {
+                            float ss = 0.0f;
+#pragma unroll
+                            for (int i = 0; i < 16; i++) {
+                                const float vv = acc[r][i] + bv[i];
+                                ss += vv * vv;
+                            }
+                            ss += __shfl_xor(ss, 32, 64);
+                            if (h == 0) red0[(mt * XP_TY + XP_ROWS * g + r) * XP_TX + j] = ss;
+                        }
+                    }
+                    __syncthreads();
+                    if (mfma_wave) {
+#pragma unroll
+                        for (int r = 0; r < XP_ROWS; r++) {
+                            const int row = XP_ROWS * g + r;
+                            const float tot = red0[row * XP_TX + j] + red0[(XP_TY + row) * XP_TX + j];
+                            const float inv = 1.0f / sqrtf(fmaxf(tot, 1e-12f));
+                            float v[16];
+                            float s2 = 0.0f;
+#pragma unroll
+                            for (int i = 0; i < 16; i++) { v[i] = (acc[r][i] + bv[i]) * inv; s2 += v[i] * v[i]; }
+                            s2 += __shfl_xor(s2, 32, 64);
+                            if (h == 0) red1[(mt * XP_TY + row) * XP_TX + j] = s2;
+                            const int y = ty0 + row, x = tx0 + j;
+                            if (y < Hout && x < Wout) {
+                                const size_t pix = (size_t)y * Wout + x;
+#pragma unroll
+                                for (int q = 0; q < 4; q++) {
+                                    const int c = mt * 32 + 8 * q + 4 * h;
+                                    *reinterpret_cast<float4 *>(out + pix * NF + c) =
+                                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                                    if (ohi) {
+                                        bf16x4 hv, lv;
+#pragma unroll
+                                        for (int e = 0; e < 4; e++) {
+                                            const float xv = v[4 * q + e];
+                                            const __bf16 hh = (__bf16)xv;
+                                            hv[e] = hh;
+                                            lv[e] = (__bf16)(xv - (float)hh);
+                                        }
+                                        *reinterpret_cast<uint2 *>(ohi + pix * NF + c) = __builtin_bit_cast(uint2, hv);
+                                        *reinterpret_cast<uint2 *>(olo + pix * NF + c) = __builtin_bit_cast(uint2, lv);
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    if (onrm && mfma_wave && mt == 0 && h == 0) {
+#pragma unroll
+                        for (int r = 0; r < XP_ROWS; r++) {
+                            const int row = XP_ROWS * g + r, y = ty0 + row, x = tx0 + j;
+                            if (y < Hout && x < Wout)   // fp32 rounding bound of the 64-term sum
+                                onrm[(size_t)y * Wout + x] =
+                                    sqrtf(red1[row * XP_TX + j] + red1[(XP_TY + row) * XP_TX + j]) * 1.000004f;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            cur ^= 1;
         }
-    } else {
-        float ss = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; r++) ss += v[0][r] * v[0][r] + v[1][r] * v[1][r];
-        ss += __shfl_xor(ss, 32, 64);
-        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-#pragma unroll
-        for (int r = 0; r < 16; r++) { v[0][r] *= inv; v[1][r] *= inv; }
     }
-    const int oy = ty0 + wave, ox = tx0 + j;
-    if (oy < Hout && ox < Wout) {
-        const size_t pix = (size_t)oy * Wout + ox;
-        float *dst = out + pix * NF;
-#pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-#pragma unroll
-            for (int g = 0; g < 4; g++)
-                *reinterpret_cast<float4 *>(dst + mt * 32 + 8 * g + 4 * h) =
-                    make_float4(v[mt][4 * g], v[mt][4 * g + 1], v[mt][4 * g + 2], v[mt][4 * g + 3]);
-        if (LAST && ohi) emit_split(v, h, pix, ohi, olo);
-    }
-    if (LAST && onrm) emit_norm(v, h, oy < Hout && ox < Wout ? (size_t)oy * Wout + ox : (size_t)-1, onrm);
 }
 
 // nlayers == 1: conv1 + L2 normalisation only (no ReLU on the last layer).
@@ -564,9 +732,12 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
                     const float r1 = x - bf2f(h0);
                     const uint16_t h1 = f2bf_rne(r1);
                     const float r2 = r1 - bf2f(h1);
-                    pl[dsti] = h0;
-                    pl[LK_W + dsti] = h1;
-                    pl[2 * (size_t)LK_W + dsti] = f2bf_rne(r2);
+                    const uint16_t parts[3] = {h0, h1, f2bf_rne(r2)};
+                    // A-fragment order [mtile][cblock][tap][part][lane][8] (conv64_x6p_kernel):
+                    // lane = (c % 16 >= 8) * 32 + n % 32, element c % 8
+                    const int mt = n >> 5, cb = c >> 4, ln = ((c >> 3) & 1) * 32 + (n & 31);
+                    for (int q = 0; q < 3; q++)
+                        pl[((((size_t)(mt * XP_NCB + cb) * 9 + tap) * 3 + q) * 64 + ln) * 8 + (c & 7)] = parts[q];
                 }
         o += LK_FLOATS;
     }
@@ -590,17 +761,40 @@ static void set_tower_attrs()
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
-    (void)hipFuncSetAttribute((const void *)conv64_x6_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_SMEM);
+#define SDE_X6P_ATTR(F, L, I, O) (void)hipFuncSetAttribute((const void *)conv64_x6p_kernel<F, L, I, O>, \
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, XP_SMEM)
+    SDE_X6P_ATTR(true, false, false, true);
+    SDE_X6P_ATTR(true, false, false, false);
+    SDE_X6P_ATTR(true, true, false, false);
+    SDE_X6P_ATTR(false, false, true, true);
+    SDE_X6P_ATTR(false, false, false, false);
+    SDE_X6P_ATTR(false, false, true, false);
+    SDE_X6P_ATTR(false, false, false, true);
+    SDE_X6P_ATTR(false, true, true, false);
+    SDE_X6P_ATTR(false, true, false, false);
+#undef SDE_X6P_ATTR
     done = true;
+}
+
+static int cu_count()
+{
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
 }
 
 // One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
 // layer > 2 -> one 64->64 conv on Hin x Win x 64 activations.  Output (Hin-4|Hin-2) x ... x 64.
+// in_cb / out_cb: activations in the c-block-major layout [4][h][w][16] (bf16x6 path only).
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
-                         int flags, uint16_t *ohi, uint16_t *olo, float *onrm, hipStream_t st)
+                         int flags, uint16_t *ohi, uint16_t *olo, float *onrm, bool in_cb, bool out_cb,
+                         hipStream_t st)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
@@ -608,16 +802,33 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     const float *w1 = packed;
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
+    if (x6) {
+        const int tiles_x = cdiv(wout, XP_TX), ntiles = tiles_x * cdiv(hout, XP_TY);
+        const int grid = std::min(ntiles, cu_count());
+#define SDE_X6P(F, L, I, O) conv64_x6p_kernel<F, L, I, O><<<grid, 512, XP_SMEM, st>>>( \
+        in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
+        (L) ? onrm : nullptr, tiles_x, ntiles)
+        if (layer == 2) {
+            if (last) SDE_X6P(true, true, false, false);
+            else if (out_cb) SDE_X6P(true, false, false, true);
+            else SDE_X6P(true, false, false, false);
+        } else if (last) {
+            if (in_cb) SDE_X6P(false, true, true, false);
+            else SDE_X6P(false, true, false, false);
+        } else {
+            if (in_cb && out_cb) SDE_X6P(false, false, true, true);
+            else if (in_cb) SDE_X6P(false, false, true, false);
+            else if (out_cb) SDE_X6P(false, false, false, true);
+            else SDE_X6P(false, false, false, false);
+        }
+#undef SDE_X6P
+        return;
+    }
     dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
 #define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, \
                                                              (L) ? ohi : nullptr, (L) ? olo : nullptr, (L) ? onrm : nullptr)
-    if (x6) {
-        if (layer == 2) { if (last) SDE_CONV(conv64_x6_kernel, true, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, true, false, X6_SMEM); }
-        else { if (last) SDE_CONV(conv64_x6_kernel, false, true, X6_SMEM); else SDE_CONV(conv64_x6_kernel, false, false, X6_SMEM); }
-    } else {
-        if (layer == 2) { if (last) SDE_CONV(conv64_mfma_kernel, true, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, true, false, TW_SMEM); }
-        else { if (last) SDE_CONV(conv64_mfma_kernel, false, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, false, false, TW_SMEM); }
-    }
+    if (layer == 2) { if (last) SDE_CONV(conv64_mfma_kernel, true, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, true, false, TW_SMEM); }
+    else { if (last) SDE_CONV(conv64_mfma_kernel, false, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, false, false, TW_SMEM); }
 #undef SDE_CONV
 }
 
@@ -627,9 +838,13 @@ SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *p
 {
     if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
     if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
-    if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
+    if (flags & ~(SDE_TOWER_BF16X6 | SDE_TOWER_IN_CBLOCK | SDE_TOWER_OUT_CBLOCK)) return SDE_ERR_ARG;
+    const bool in_cb = (flags & SDE_TOWER_IN_CBLOCK) != 0, out_cb = (flags & SDE_TOWER_OUT_CBLOCK) != 0;
+    if ((in_cb || out_cb) && !(flags & SDE_TOWER_BF16X6)) return SDE_ERR_ARG;
+    if ((in_cb && layer == 2) || (out_cb && layer == nlayers)) return SDE_ERR_ARG;
     if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
-    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, as_stream(stream));
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, in_cb, out_cb,
+                 as_stream(stream));
     return launch_status();
 }
 
@@ -656,13 +871,16 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
         buf[1] = buf[0] + h2 * w2 * NF;
     }
     int hin = Hp, win = Wp;
+    // intermediate activations in the c-block-major layout on the bf16x6 path
+    const bool cbl = (flags & SDE_TOWER_BF16X6) != 0;
     launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, feat_hi, feat_lo, feat_norm,
-                 st);
+                 false, cbl && nlayers > 2, st);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
-        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, st);
+        launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, cbl,
+                     cbl && l < nlayers, st);
         hin -= 2; win -= 2;
         cur ^= 1;
     }

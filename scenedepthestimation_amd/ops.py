@@ -270,8 +270,17 @@ def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspa
     return out
 
 
-def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None):
-    """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image)."""
+def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
+                in_cblock: bool = False, out_cblock: bool = False):
+    """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
+    in_cblock / out_cblock (bf16x6): intermediate activations in the c-block-major layout
+    [nf/16][h][w][16] that tower_forward uses between layers (tensors keep their [h, w, nf]
+    shape; only the element order differs)."""
+    flags = TOWER_PRECISIONS[precision]
+    if in_cblock:
+        flags |= _lib.SDE_TOWER_IN_CBLOCK
+    if out_cblock:
+        flags |= _lib.SDE_TOWER_OUT_CBLOCK
     if layer == 2:
         Hin, Win = inp.shape
         oshape = (Hin - 4, Win - 4, nf)
@@ -281,7 +290,7 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precis
     check(lib.sde_tower_layer(_need(inp, "layer input"), Hin, Win,
                               _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
                               nlayers, nf, layer, _need(out, "layer output", shape=oshape),
-                              TOWER_PRECISIONS[precision], *_split_ptrs(split, oshape[:2]), _stream()),
+                              flags, *_split_ptrs(split, oshape[:2]), _stream()),
           "sde_tower_layer")
     return out
 

@@ -40,7 +40,7 @@ def test_tower_packing_matches_layout():
     hw, hb = mc_cnn.layer_lists(w, L)
     packed = ops.pack_tower_weights(hw, hb)
     LW = 9 * 64 * 64
-    LK = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 planes
+    LK = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 parts
     assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * LK
     assert np.array_equal(packed[:64], hb[0])
     assert np.array_equal(packed[64:640], hw[0].reshape(-1))
@@ -50,9 +50,13 @@ def test_tower_packing_matches_layout():
         blob = packed[base + 64:base + 64 + LW].reshape(9, 64, 64)            # [tap][n][c]
         ref = hw[l].reshape(9, 64, 64).transpose(0, 2, 1)                     # HWIO [tap][c][n] -> [tap][n][c]
         assert np.array_equal(blob, ref)
-        # the three bf16 planes sum exactly to the fp32 weight (RNE splits, exact residuals)
-        planes = packed[base + 64 + LW:base + LK].view(np.uint16).reshape(3, 9, 64, 64)
+        # bf16 parts in A-fragment order [mtile 2][cblock 4][tap 9][part 3][lane 64][8]:
+        # lane = ((c % 16) >= 8) * 32 + n % 32, element c % 8 (conv64_x6p_kernel)
+        frag = packed[base + 64 + LW:base + LK].view(np.uint16).reshape(2, 4, 9, 3, 2, 32, 8)
+        # -> [part][tap][n = mt*32 + lane%32][c = cb*16 + half*8 + e]
+        planes = frag.transpose(3, 2, 0, 5, 1, 4, 6).reshape(3, 9, 64, 64)
         as_f32 = (planes.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        # the three bf16 parts sum exactly to the fp32 weight (RNE splits, exact residuals)
         assert np.array_equal(as_f32.sum(0), ref.astype(np.float64))
         hi = as_f32[0]
         assert np.all(np.abs(ref - hi) <= np.abs(ref) * 2.0 ** -8)

@@ -170,6 +170,48 @@ def test_tower_precision_report(gpu, oracle):
     assert errs["fp32"] < 1e-5 and errs["bf16x6"] < 1e-5
 
 
+@pytest.mark.parametrize("nlayers,H,W", [(5, 700, 530), (3, 300, 1100), (2, 530, 517)])
+def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W):
+    """Sizes with more output tiles than CUs (the persistent bf16x6 kernel's tile loop, partial
+    edge tiles, the c-block-major intermediate layout): bf16x6 vs the fp32-MFMA kernel, both
+    fp32-level accurate, agree to ~1e-6."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    rng = np.random.default_rng(H + W)
+    w = mc_cnn.synthetic_weights(nlayers, seed=3)
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(w, nlayers)))
+    img = torch.zeros((H + 2 * nlayers, W + 2 * nlayers), device="cuda")
+    img[nlayers:-nlayers, nlayers:-nlayers] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
+    a = ops.tower_forward(img, packed, nlayers, precision="fp32")
+    b = ops.tower_forward(img, packed, nlayers, precision="bf16x6")
+    torch.cuda.synchronize()
+    assert torch.isfinite(b).all()
+    err = float((a - b).abs().max())
+    print("bf16x6 vs fp32 tower", (nlayers, H, W), err)
+    assert err < 1e-5
+
+
+def test_tower_layer_api_matches_forward(gpu):
+    """sde_tower_layer ([h][w][64] in/out) chained layer by layer == sde_tower_forward."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    L, H, W = 5, 150, 610
+    rng = np.random.default_rng(5)
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=9), L)))
+    img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
+    img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
+    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True)):
+        full = ops.tower_forward(img, packed, L, precision=prec)
+        x = img
+        for layer in range(2, L + 1):
+            shrink = 4 if layer == 2 else 2
+            y = torch.empty((x.shape[0] - shrink, x.shape[1] - shrink, 64), device="cuda")
+            ops.tower_layer(x, packed, L, layer, y, precision=prec, in_cblock=cbl and layer > 2,
+                            out_cblock=cbl and layer < L)
+            x = y
+        torch.cuda.synchronize()
+        # same arithmetic in the same order whatever the activation layout: bit-identical
+        assert torch.equal(x, full), (prec, cbl)
+
+
 def test_preprocess_u8(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(8)
