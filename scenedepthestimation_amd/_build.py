@@ -29,6 +29,13 @@ HIPCC_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-con
                "-fvisibility=hidden", "-Wall", "-Wno-unused-function", "-I" + INCLUDE, "-I" + CSRC]
 
 
+# cv_row.hip: the certified row-sweep kernel's per-score max / median / compare run without
+# NaN canonicalisation (IEEE mode off).  Its certificate takes every decision that must survive
+# non-finite input on integer bit tests, and its exact arithmetic (no NaN, no contraction) is
+# unaffected; nothing else is built this way.
+PER_FILE_FLAGS = {"cv_row.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):
@@ -51,7 +58,7 @@ def _compile(src: str, force: bool) -> str:
     if not force and os.path.exists(obj) and \
             os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime()):
         return obj
-    cmd = [hipcc()] + HIPCC_FLAGS + ["-c", src, "-o", obj]
+    cmd = [hipcc()] + HIPCC_FLAGS + PER_FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")

@@ -20,6 +20,7 @@
 // [16w, 16w+16) of each chunk; the fused WTA merges the 4 per-wave first-minima
 // by (value, index) at the end, which equals the sequential scan.
 #include "sde_common.h"
+#include "cv_cert.h"
 
 #include <algorithm>
 
@@ -295,60 +296,10 @@ __global__ __launch_bounds__(256) void argmin_merge_kernel(const float *__restri
 // Blocks are remapped so all blocks of a row run on one XCD (its L2 serves the
 // overlapping windows).
 // ===========================================================================
-typedef __bf16 fx_bf16x8 __attribute__((ext_vector_type(8)));
-typedef float fx_floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int FX_NX = 64;          // left pixels per workgroup
-constexpr int FX_DCH = 128;        // disparities per window chunk
-constexpr int FX_NT = 6;           // max M-tiles per chunk: ceil((128 + 63) / 32)
-constexpr int FX_WIN = FX_NT * 32; // window pixels
-constexpr float FX_K = 1e-4f;
-constexpr float FX_ABS = 1e-30f;   // absolute slack (bf16 subnormal handling)
-
-// Exact NumPy-order cost of two 64-float rows in global memory (16-B loads).
-__device__ __forceinline__ float dot64_exact_global(const float4 *__restrict__ a, const float4 *__restrict__ b)
-{
-    float acc[8];
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-        const float4 a0 = a[2 * m], a1 = a[2 * m + 1], b0 = b[2 * m], b1 = b[2 * m + 1];
-        const float p[8] = {a0.x * b0.x, a0.y * b0.y, a0.z * b0.z, a0.w * b0.w,
-                            a1.x * b1.x, a1.y * b1.y, a1.z * b1.z, a1.w * b1.w};
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) acc[jj] = (m == 0) ? p[jj] : acc[jj] + p[jj];
-    }
-    const float res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-    return -(0.0f + res);
-}
-
-__device__ __forceinline__ int fx_slot(int r, int c8) { return r * 8 + (c8 ^ ((r >> 1) & 7)); }
-
-__device__ __forceinline__ void fx_split(float x, __bf16 &h, __bf16 &l)
-{
-    h = (__bf16)x;
-    l = (__bf16)(x - (float)h);
-}
-
-// merge (best, arg, second) of two disjoint candidate sets, scores in max-domain
-__device__ __forceinline__ void fx_merge(float &b, int &a, float &s, float b2, int a2, float s2)
-{
-    const float ns = fmaxf(fminf(b, b2), fmaxf(s, s2));
-    if (b2 > b || (b2 == b && a2 < a)) { b = b2; a = a2; }
-    s = ns;
-}
-
-__device__ __forceinline__ int xcd_remap(int b, int nb)
-{
-    // bijective: blocks b, b+8, ... (one XCD under round-robin dispatch) get consecutive logical ids
-    const int q = nb / 8, r = nb % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
 // Split of a feature map for the certified path: x = hi + lo + r with hi =
 // bf16_rne(x), lo = bf16_rne(x - hi) (|r| <= 2^-16 |x|), plus an upper bound of
 // each pixel's L2 norm (fp32 sum of 64 squares, relative error <= 64*2^-24,
 // inflated by (1 + 4e-6)).  16 lanes per pixel, one float4 each.
-constexpr float FX_NORM_UP = 1.000004f;
 
 __global__ __launch_bounds__(256) void feature_split_kernel(const float *__restrict__ f, int64_t npix,
                                                             uint16_t *__restrict__ hi, uint16_t *__restrict__ lo,
@@ -534,6 +485,7 @@ __global__ __launch_bounds__(256) void cv_wta_cert_kernel(const float *__restric
     }
 }
 
+
 // Exact resolution of the listed pixels: one wave per pixel, lanes split the
 // d range (increasing d per lane), then a (value, index) merge == sequential scan.
 __global__ __launch_bounds__(256) void cv_wta_fixup_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
@@ -551,10 +503,22 @@ __global__ __launch_bounds__(256) void cv_wta_fixup_kernel(const float *__restri
         const float4 *a = reinterpret_cast<const float4 *>(fl + p * 64);
         float best = __builtin_inff();
         int arg = -1;
-        for (int d = d0 + lane; d < d1; d += 64) {
-            float cost = -0.0f;
-            if (x >= d) cost = dot64_exact_global(a, reinterpret_cast<const float4 *>(fr + (rowbase + x - d) * 64));
-            if (cost < best) { best = cost; arg = d; }
+        // four disparities per lane in flight at once (their row loads overlap), then the
+        // in-order first-min scan over them
+        for (int db = d0 + lane; db < d1; db += 256) {
+            float c4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int d = db + 64 * u;
+                const int xr = x - d;
+                const float cv = dot64_exact_global(a, reinterpret_cast<const float4 *>(fr + (rowbase + (xr >= 0 ? xr : 0)) * 64));
+                c4[u] = (d < d1 && xr >= 0) ? cv : -0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int d = db + 64 * u;
+                if (d < d1 && c4[u] < best) { best = c4[u]; arg = d; }
+            }
         }
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -696,7 +660,15 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
     if (!disp && !min_cost && !argmin) return SDE_ERR_ARG;
     if (mode != SDE_CV_EXACT && mode != SDE_CV_CERTIFIED) return SDE_ERR_ARG;
     hipStream_t st = as_stream(stream);
-    if (C == 64 && mode == SDE_CV_CERTIFIED) {
+    if (C == 64 && mode == SDE_CV_CERTIFIED && row_cert_supported(d0, d1)) {
+        // row-sweep kernel straight from the fp32 features (cv_row.hip)
+        if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
+        unsigned *counter = reinterpret_cast<unsigned *>(workspace);
+        int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
+        if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+        launch_row_cert(fl, fr, H, W, d0, d1, min_cost, argmin, disp, counter, list, st);
+        cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
+    } else if (C == 64 && mode == SDE_CV_CERTIFIED) {
         if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
         const int64_t npix = (int64_t)H * W;
         char *base = reinterpret_cast<char *>(workspace) + cert_ws_bytes(H, W, false);

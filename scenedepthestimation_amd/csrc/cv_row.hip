@@ -1,0 +1,307 @@
+// cv_row.hip -- row-sweep certified fused cost volume + WTA (north-star kernel).
+//
+// Replaces (WHDY/SceneDepthEstimation) compute_cost_volume + WTA1,
+// process_functional.py:48-73 + 96-113, fused: the disparity map is bit-identical
+// to WTA1(compute_cost_volume(fl, fr, D)) (see cv_cert.h / cost_volume.hip for the
+// certificate).  Built with -fno-honor-nans -mno-amdgpu-ieee (see _build.py): the
+// per-score max / median / compare run without NaN canonicalisation, so every
+// decision that must survive non-finite input is taken on integer bit tests.
+#include "cv_cert.h"
+
+#include <algorithm>
+
+namespace sde {
+
+// ---------------------------------------------------------------------------
+// Row-sweep certified CV + WTA on fp32 features (cv_wta_row_kernel).
+//
+// One 512-thread workgroup per image row walks the row in 256-pixel superstrips;
+// wave w owns the 32 left pixels [256k + 32w, +32) (one MFMA N-tile) and sweeps
+// every right tile of its disparity band itself, so a pixel's best / runner-up /
+// argmin never leave the wave (no cross-wave merge).  The right-feature window of
+// a superstrip (256 + D - 1 pixels, in 32-pixel tiles) lives in an LDS ring of
+// hi/lo bf16 planes; advancing one superstrip retires 8 tiles and admits 8, so
+// every right pixel is read from HBM once per row (the chunked kernel above
+// re-stages ~5x the window).  New tiles are loaded one superstrip ahead into
+// registers, then split into hi/lo (and their pixel norms and per-tile norm
+// maximum computed) by the threads that loaded them: no pre-split pass -- the
+// kernel's only HBM input is the two fp32 feature maps (the algorithmic minimum).
+// Left operands are prefetched one superstrip ahead and split in registers.
+// 12 MFMAs per 32x32 tile pair, then the certificate of cv_wta_cert_kernel: a
+// pixel whose best fast score beats the runner-up by more than 2 eps gets its
+// exact cost recomputed from the fp32 rows (L2-resident) when requested, the rest
+// go to the fix-up list.  Outputs are bit-identical to the exact kernel.  Tiles
+// left of the image are zero-filled, so an invalid voxel (x < d) scores exactly
+// +0 = -(-0.0), like the CPU path.
+// ---------------------------------------------------------------------------
+constexpr int RW_T = 32;           // pixels per tile (= one MFMA N-tile of left pixels)
+constexpr int RW_WAVES = 8;
+constexpr int RW_NX = RW_T * RW_WAVES;   // left pixels per superstrip (256)
+constexpr int RW_NEW = RW_NX / RW_T;     // tiles admitted per superstrip (8)
+
+__device__ __forceinline__ int rw_slot(int T, int nt) { return ((T % nt) + nt) % nt; }
+
+// one 16-B unit (pixel u>>4, channels 4(u&15)..+3) of right tile T (zero outside the row)
+__device__ __forceinline__ float4 rw_load(const float *__restrict__ frrow, int W, int T, int u)
+{
+    const int xr = T * RW_T + (u >> 4);
+    const bool ok = xr >= 0 && xr < W;
+    const float4 v = reinterpret_cast<const float4 *>(frrow)[(size_t)(ok ? xr : 0) * 16 + (u & 15)];
+    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ bool rw_nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
+
+// split one unit into the ring slot's hi/lo planes; the pixel's 16 lanes reduce its squared norm
+// and the tile's 32 pixels (512 units = 8 waves x 64 lanes -> 4 pixels per wave) its maximum
+// (tmax) and whether any channel is non-finite (tbad).  Integer tests: this file is built with
+// relaxed NaN handling, which may not be trusted to keep float NaN tests.
+__device__ __forceinline__ void rw_store(uint4 *ring, unsigned *tmax, unsigned *tbad, int slot, int u, float4 v)
+{
+    const int px = u >> 4, q = u & 15;
+    __bf16 h0, h1, h2, h3, l0, l1, l2, l3;
+    fx_split(v.x, h0, l0); fx_split(v.y, h1, l1); fx_split(v.z, h2, l2); fx_split(v.w, h3, l3);
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const bf4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+    char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
+    *reinterpret_cast<uint2 *>(base) = __builtin_bit_cast(uint2, hv);
+    *reinterpret_cast<uint2 *>(base + 256 * 16) = __builtin_bit_cast(uint2, lv);
+    float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    ss += __shfl_xor(ss, 4, 64);
+    ss += __shfl_xor(ss, 8, 64);
+    // squared norms are non-negative: their bit patterns order like unsigned integers
+    unsigned nb = __float_as_uint(ss);
+    nb = max(nb, (unsigned)__shfl_xor((int)nb, 16, 64));
+    nb = max(nb, (unsigned)__shfl_xor((int)nb, 32, 64));
+    const bool bad = rw_nonfinite(v.x) || rw_nonfinite(v.y) || rw_nonfinite(v.z) || rw_nonfinite(v.w);
+    const uint64_t anybad = __ballot(bad);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&tmax[slot], nb);
+        if (anybad) atomicOr(&tbad[slot], 1u);
+    }
+}
+
+template <bool WANT_MIN>
+__global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                         int H, int W, int d0, int d1, int tlo0, int ntw,
+                                                         float *__restrict__ out_min, int32_t *__restrict__ out_arg,
+                                                         float *__restrict__ out_disp, unsigned *__restrict__ counter,
+                                                         int32_t *__restrict__ list)
+{
+    extern __shared__ __attribute__((aligned(16))) uint4 rsm[];
+    uint4 *ring = rsm;                                              // [ntw][2 planes][32 px][8 chunks]
+    unsigned *tmax = reinterpret_cast<unsigned *>(ring + ntw * 512); // [ntw] max squared pixel norm (f32 bits)
+    unsigned *tbad = tmax + ntw;                                    // [ntw] any non-finite channel
+
+    const int y = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile loop runs on SALU
+    const int j = lane & 31, h = lane >> 5;
+    const float *flrow = fl + (size_t)y * W * 64;
+    const float *frrow = fr + (size_t)y * W * 64;
+    const size_t rowpix = (size_t)y * W;
+    const int nss = (W + RW_NX - 1) / RW_NX;
+
+    // prologue: the first superstrip's window
+    for (int i = tid; i < ntw; i += 512) { tmax[i] = 0u; tbad[i] = 0u; }
+    __syncthreads();
+    {
+        // all loads in flight before the first store (a load -> store chain per tile would serialise
+        // ntw HBM latencies)
+        constexpr int MAXT = 18;
+        float4 pv[MAXT];
+#pragma unroll
+        for (int t = 0; t < MAXT; t++)
+            if (t < ntw) pv[t] = rw_load(frrow, W, tlo0 + t, tid);
+#pragma unroll
+        for (int t = 0; t < MAXT; t++)
+            if (t < ntw) rw_store(ring, tmax, tbad, rw_slot(tlo0 + t, ntw), tid, pv[t]);
+    }
+    // left operand (raw fp32: channels 16s+8h..+7 of pixel x), prefetched one superstrip ahead
+    float4 lraw[8];
+    auto load_left = [&](int kk) {
+        const int xx = kk * RW_NX + RW_T * wave + j;
+        const float4 *src = reinterpret_cast<const float4 *>(flrow) + (size_t)(xx < W ? xx : 0) * 16 + 2 * h;
+#pragma unroll
+        for (int s = 0; s < 4; s++) { lraw[2 * s] = src[4 * s]; lraw[2 * s + 1] = src[4 * s + 1]; }
+    };
+    load_left(0);
+    __syncthreads();
+
+    for (int k = 0; k < nss; k++) {
+        const int tlo = tlo0 + RW_NEW * k;
+        const bool more = k + 1 < nss;
+        // the next superstrip's 8 new tiles: loaded now, stored after this superstrip's reads
+        float4 nv[RW_NEW];
+#pragma unroll
+        for (int t = 0; t < RW_NEW; t++)
+            nv[t] = more ? rw_load(frrow, W, tlo + ntw + t, tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+
+        const int xb = k * RW_NX + RW_T * wave;
+        const int x = xb + j;
+        const bool xok = x < W;
+        float best = -__builtin_inff(), second = -__builtin_inff();
+        int arg = -1;
+        float nl = 0.0f;
+        unsigned nmax2 = 0u, wbad = 0u;     // window: max squared norm (bits), any non-finite tile
+        bool lbad = false;
+        if (xb < W) {          // wave-uniform: waves past the row end only help with the ring
+            fx_bf16x8 bh[4], bl[4];
+            float ssl = 0.0f;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const float4 a = lraw[2 * s], b = lraw[2 * s + 1];
+                const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    __bf16 hh, ll;
+                    fx_split(v8[e], hh, ll);
+                    bh[s][e] = hh;
+                    bl[s][e] = ll;
+                    ssl += v8[e] * v8[e];
+                    lbad |= rw_nonfinite(v8[e]);
+                }
+            }
+            ssl += __shfl_xor(ssl, 32, 64);
+            lbad |= __shfl_xor((int)lbad, 32, 64) != 0;
+            nl = sqrtf(ssl) * FX_NORM_UP;
+            if (more) load_left(k + 1);
+
+            float b1[4], b2[4];
+            int ag[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) { b1[t] = -__builtin_inff(); b2[t] = -__builtin_inff(); ag[t] = -1; }
+            // right tiles of this N-tile's band: d = x - xr in [d0, d1)
+            // right pixels xr in [xb - d1 + 1, xb + 31 - d0]: tiles floor(./32) (offset keeps it non-negative)
+            const int Ta = (xb - d1 + 1 + RW_T * 4096) / RW_T - 4096;
+            const int Tb = (xb + 31 - d0 + RW_T * 4096) / RW_T - 4096;
+            const int T0 = max(Ta, tlo), T1 = min(Tb, tlo + ntw - 1);
+            int slot = rw_slot(T0, ntw);                   // advanced incrementally (no division per tile)
+            for (int T = T0; T <= T1; T++, slot = (slot + 1 == ntw) ? 0 : slot + 1) {
+                const int dt = xb - RW_T * T;
+                const int dlo = dt - 31, dhi = dt + 31;
+                if (dhi < d0 || dlo >= d1) continue;     // wave-uniform
+                nmax2 = max(nmax2, tmax[slot]);
+                wbad |= tbad[slot];
+                const uint4 *tp = ring + slot * 512;
+                fx_floatx16 acc = {0};
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int sl = fx_slot(j, 2 * s + h);
+                    const fx_bf16x8 ah = __builtin_bit_cast(fx_bf16x8, tp[sl]);
+                    const fx_bf16x8 al = __builtin_bit_cast(fx_bf16x8, tp[256 + sl]);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+                }
+                const int dl = dt + j - 4 * h;             // d of register r is dl - ((r&3) + 8(r>>2))
+                if (dlo >= d0 && dhi < d1) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int t = r & 3;
+                        const int d = dl - ((r & 3) + 8 * (r >> 2));
+                        const float sc = acc[r];
+                        const bool gt = sc > b1[t];
+                        ag[t] = gt ? d : ag[t];
+                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                        b1[t] = fmaxf(b1[t], sc);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int t = r & 3;
+                        const int d = dl - ((r & 3) + 8 * (r >> 2));
+                        const float sc = (d >= d0 && d < d1) ? acc[r] : -__builtin_inff();
+                        const bool gt = sc > b1[t];
+                        ag[t] = gt ? d : ag[t];
+                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                        b1[t] = fmaxf(b1[t], sc);
+                    }
+                }
+            }
+            best = b1[0]; second = b2[0]; arg = ag[0];
+#pragma unroll
+            for (int t = 1; t < 4; t++) fx_merge(best, arg, second, b1[t], ag[t], b2[t]);
+            {
+                const float bb = __shfl_xor(best, 32, 64), ss2 = __shfl_xor(second, 32, 64);
+                const int aa = __shfl_xor(arg, 32, 64);
+                fx_merge(best, arg, second, bb, aa, ss2);
+            }
+        }
+        __syncthreads();       // every wave is done reading the retiring tiles
+        if (more) {
+            for (int t = tid; t < RW_NEW; t += 512) {
+                tmax[rw_slot(tlo + ntw + t, ntw)] = 0u;
+                tbad[rw_slot(tlo + ntw + t, ntw)] = 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < RW_NEW; t++) rw_store(ring, tmax, tbad, rw_slot(tlo + ntw + t, ntw), tid, nv[t]);
+        }
+        // certificate and outputs (off the ring: overlaps the stores)
+        if (xb < W && h == 0 && xok) {
+            const float eps = FX_K * nl * (sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP) + FX_ABS;
+            const size_t p = rowpix + x;
+            // certified only when every operand is finite (then every score and eps are finite too)
+            if (!lbad && !wbad && (best - second) > 2.0f * eps && arg >= 0) {
+                if (WANT_MIN) {
+                    float cost = -0.0f;
+                    if (x - arg >= 0)
+                        cost = dot64_exact_global(reinterpret_cast<const float4 *>(flrow + (size_t)x * 64),
+                                                  reinterpret_cast<const float4 *>(frrow + (size_t)(x - arg) * 64));
+                    out_min[p] = cost;
+                }
+                if (out_arg) out_arg[p] = arg;
+                if (out_disp) out_disp[p] = (float)arg;
+            } else {
+                // near-ties and non-finite operands: the IEEE fix-up kernel's exact scan
+                list[atomicAdd(counter, 1u)] = (int32_t)p;
+            }
+        }
+        __syncthreads();
+    }
+
+}
+
+// tiles spanned by a superstrip's window and the first one (superstrip 0), floor division
+static void row_window(int d0, int d1, int &tlo0, int &ntw)
+{
+    auto fdiv = [](int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+    tlo0 = fdiv(-(d1 - 1), RW_T);
+    const int thi0 = fdiv(RW_NX - 1 - d0, RW_T);
+    ntw = thi0 - tlo0 + 1;
+}
+
+static size_t row_smem(int ntw) { return (size_t)ntw * 512 * 16 + (size_t)ntw * 8; }
+
+bool row_cert_supported(int d0, int d1)
+{
+    int tlo0 = 0, ntw = 0;
+    row_window(d0, d1, tlo0, ntw);
+    return ntw <= 18;
+}
+
+void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int d1, float *out_min, int32_t *out_arg,
+                     float *out_disp, unsigned *counter, int32_t *list, hipStream_t st)
+{
+    int tlo0 = 0, ntw = 0;
+    row_window(d0, d1, tlo0, ntw);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  150 * 1024);
+        (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  150 * 1024);
+        attr = true;
+    }
+    if (out_min)
+        cv_wta_row_kernel<true><<<H, 512, row_smem(ntw), st>>>(fl, fr, H, W, d0, d1, tlo0, ntw, out_min, out_arg,
+                                                               out_disp, counter, list);
+    else
+        cv_wta_row_kernel<false><<<H, 512, row_smem(ntw), st>>>(fl, fr, H, W, d0, d1, tlo0, ntw, nullptr, out_arg,
+                                                                out_disp, counter, list);
+}
+
+}  // namespace sde

@@ -25,7 +25,8 @@ from . import mc_cnn, ops
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
                  nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6",
-                 cv_mode: str = "certified", cbca_iters: int = 0, cbca_L1: int = 14, cbca_tau: float = 0.02):
+                 cv_mode: str = "certified", cbca_iters: int = 0, cbca_L1: int = 14, cbca_tau: float = 0.02,
+                 emit_split: bool = False):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)
         # cross-based aggregation before SGM (build-defined stage; 0 = the reference's GPU path)
         self.cbca_iters, self.cbca_L1, self.cbca_tau = int(cbca_iters), int(cbca_L1), float(cbca_tau)
@@ -52,9 +53,11 @@ class StereoMatcher:
         self.argmin = torch.empty((H, W), dtype=torch.int32, device=dev)
         self.cv_mode = cv_mode
         self.cv_ws = torch.empty(ops.cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device=dev)
-        # bf16 split planes + norm bounds emitted by the tower's last layer (certified cost volume input)
-        self.split = [ops.new_split(H, W, dev) for _ in range(2)] if (cv_mode == "certified" and nlayers >= 2) \
-            else None
+        # optional: bf16 split planes + norm bounds emitted by the tower's last layer, consumed by
+        # sde_cv_wta_split.  The default certified path (sde_cv_wta, row-sweep kernel) splits the fp32
+        # features itself and reads nothing else, so the planes are not written by default.
+        self.split = [ops.new_split(H, W, dev) for _ in range(2)] \
+            if (emit_split and cv_mode == "certified" and nlayers >= 2) else None
         self.split_valid = False
         self.sgm_bufs = None
         if sgm:
@@ -85,8 +88,9 @@ class StereoMatcher:
         return self.feat[0], self.feat[1]
 
     def cost_wta(self, want=("disp",)):
-        """Fused cost volume + WTA over this matcher's disparity range [d0, d1).  In certified mode the
-        tower-emitted split planes are used when the current features came from this matcher's tower."""
+        """Fused cost volume + WTA over this matcher's disparity range [d0, d1).  In certified mode with
+        emit_split=True the tower-emitted split planes are used (sde_cv_wta_split) when the current
+        features came from this matcher's tower; otherwise sde_cv_wta reads the fp32 features."""
         if self.cv_mode == "certified" and self.split_valid:
             return ops.cv_wta_split(self.feat[0], self.feat[1], self.split[0], self.split[1], self.d0, self.d1,
                                     disp=self.disp if "disp" in want else None,
