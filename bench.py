@@ -301,13 +301,14 @@ def main():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        ops.sgm_8path_pair(b["cv"][0], b["pen"][0], b["S"][0], b["cv"][1], b["pen"][1], b["S"][1],
-                           zero_du_penalties=True)
+        ops.sgm_8path_wta_pair(b["cv"][0], b["pen"][0], b["S"][0], b["disp"][0], b["cv"][1], b["pen"][1],
+                               b["S"][1], b["disp"][1], zero_du_penalties=True)
         e1.record()
         torch.cuda.synchronize()
         sgm_ms = e0.elapsed_time(e1)
-        # per side: UD+DU pass reads C, writes S (8 B/voxel); 6 more passes read C, S and write S (12 B)
-        sgm_bytes = 2 * 80.0 * vox
+        # per side: UD+DU pass reads C, writes S (8 B/voxel); 5 passes read C, S and write S (12 B);
+        # the last pass (WTA fused) reads C, S (8 B) and writes 4 B per pixel
+        sgm_bytes = 2 * (76.0 * vox + 4.0 * H * W)
         tmp = b["cbca_tmp"]
         e0.record()
         ops.cbca(b["cv"][0], b["arms"][0], b["arms"][1], "left", CBCA_L1, 1, tmp=tmp)
@@ -318,11 +319,12 @@ def main():
         stages["cbca_iter_hbm_GBs"] = 16.0 * vox / (cb_ms * 1e-3) / 1e9     # 2 passes x (read + write) x 4 B
         stages["sgm_pair_ms"] = sgm_ms
         ach = sgm_bytes / (sgm_ms * 1e-3) / 1e9
-        roof = {"kernel": "sgm_scan_kernel (8-path SGM, both sides, 7 launches: DU folded into UD)", "bound": "hbm",
+        roof = {"kernel": "sgm_scan_kernel (8-path SGM + WTA, both sides, 7 launches: DU folded into UD, WTA "
+                          "into DU-RL)", "bound": "hbm",
                 "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                 "traffic": None,
-                "per_launch": f"2 sides x (8 + 6 x 12) B/voxel x {vox / 1e6:.0f} Mvox = {sgm_bytes / 1e9:.2f} GB "
-                              f"over {sgm_ms:.3f} ms (7 launches)"}
+                "per_launch": f"2 sides x (8 + 5 x 12 + 8) B/voxel x {vox / 1e6:.0f} Mvox + disp = "
+                              f"{sgm_bytes / 1e9:.2f} GB over {sgm_ms:.3f} ms (7 launches)"}
     elif args.mode == "pairdp" or world == 1:
         cv_ms = t_cv.mean_ms()
         bytes_cv = 4.0 * H * W * 2 * NF + 4.0 * H * W

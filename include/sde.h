@@ -224,6 +224,17 @@ int sde_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float 
 int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r, const float *pen_r,
                        float *S_r, int H, int W, int D, int flags, void *stream);
 
+/*
+ * sde_sgm_8path_pair fused with WTA_and_SupixelRefinement_kernel (process_functional.py:800-837,
+ * the same first-min rule as sde_wta(..., SDE_WTA_INIT_D0)): the last direction (DU-RL) reduces
+ * each pixel's final S to its disparity in disp [H][W] float32 instead of storing S, so on
+ * return S holds the sum of the first seven directions.  disp_r may be NULL only with the
+ * right triple.  Same flags and values as sde_sgm_8path_pair followed by sde_wta.
+ */
+int sde_sgm_8path_wta_pair(const float *cv_l, const float *pen_l, float *S_l, float *disp_l, const float *cv_r,
+                           const float *pen_r, float *S_r, float *disp_r, int H, int W, int D, int flags,
+                           void *stream);
+
 /* One direction (0..7 in the order above) of sde_sgm_8path. */
 int sde_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int direction, float *S,
                       void *stream);

@@ -58,6 +58,7 @@ SIGNATURES = {
                                   c_void_p]),
     "sde_sgm_8path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_sgm_8path_pair": (c_int, [c_void_p] * 6 + [c_int, c_int, c_int, c_int, c_void_p]),
+    "sde_sgm_8path_wta_pair": (c_int, [c_void_p] * 8 + [c_int, c_int, c_int, c_int, c_void_p]),
     "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_cbca_arms": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]),
     "sde_cbca": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p]),

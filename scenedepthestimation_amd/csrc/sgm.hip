@@ -99,7 +99,56 @@ struct SgmSide {
     const float *cv;
     const float *pen;
     float *S;
+    float *disp;    // WTA fused into the last direction (sde_sgm_8path_wta_pair), else unused
 };
+
+// DPP move of an int; lanes outside ROW_MASK keep `v`.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i32(int v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, ROW_MASK, 0xF, false);
+}
+
+// first-min merge of (value, index): b replaces a iff strictly smaller, or equal with a
+// lower index -- the sequential `v < best` scan over increasing d (NaN never wins)
+__device__ __forceinline__ void wta_merge(float &v, int &a, float v2, int a2)
+{
+    if (v2 < v || (v2 == v && a2 < a)) { v = v2; a = a2; }
+}
+
+// (min, first argmin) over the 64 lanes, valid in lane 63 (same DPP butterfly as wave_min_f64)
+__device__ __forceinline__ void wave_argmin(float &v, int &a)
+{
+#define SDE_WTA_STEP(CTRL, RM)                                                               \
+    {                                                                                        \
+        const float v2 = __int_as_float(dpp_i32<CTRL, RM>(__float_as_int(v)));               \
+        const int a2 = dpp_i32<CTRL, RM>(a);                                                 \
+        wta_merge(v, a, v2, a2);                                                             \
+    }
+    SDE_WTA_STEP(0xB1, 0xF)
+    SDE_WTA_STEP(0x4E, 0xF)
+    SDE_WTA_STEP(0x124, 0xF)
+    SDE_WTA_STEP(0x128, 0xF)
+    SDE_WTA_STEP(0x142, 0xA)
+    SDE_WTA_STEP(0x143, 0xC)
+#undef SDE_WTA_STEP
+}
+
+// WTA_and_SupixelRefinement_kernel (process_functional.py:800-837) on one pixel whose S values
+// are o[i] at d = dbase + i: best = S(0), `best > S(d)` for d = 1.. (== the +inf first-min scan,
+// except that "no winner" and a NaN S(0) give 0); lane 63 holds the answer.
+template <int DPL>
+__device__ __forceinline__ int wta_pixel(const float (&o)[DPL], int dbase, int D)
+{
+    float best = __builtin_inff();
+    int arg = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < DPL; i++)
+        if (dbase + i < D && o[i] < best) { best = o[i]; arg = dbase + i; }
+    wave_argmin(best, arg);
+    const float v0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(o[0]), 0));
+    return (arg == 0x7fffffff || v0 != v0) ? 0 : arg;
+}
 
 template <int DPL>
 struct Slot {
@@ -179,7 +228,11 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
 // writes them (:134-262) -- and finite costs, DU's recurrence collapses: b = m' exactly,
 // so L_DU = C at its first pixel (row H-1) and C + 0.0 elsewhere; the reference adds
 // it after UD (launch order :1166-1203), which per voxel is this same sequence.
-template <int DPL, int PF, bool VEC, bool FIRST, bool DU>
+// WTA (last direction only): the final S of each visited voxel is not stored; the pixel's
+// first-min disparity (rule of WTA_and_SupixelRefinement_kernel) goes to sd.disp instead, and
+// the pixels this direction never visits (its lines stop one short) take the WTA of the S
+// already in memory.
+template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA>
 __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
     const SgmSide sd = blockIdx.y ? s1 : s0;
@@ -192,6 +245,10 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     const int lane = threadIdx.x;
     const int dbase = lane * DPL;
     const double INF = __builtin_inf();
+    // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block)
+    __shared__ float wbv[WTA ? PF * 64 : 1];
+    __shared__ int wba[WTA ? PF * 64 : 1];
+    __shared__ int wpx[WTA ? PF : 1];
 
     // Every load is unconditional (steps past the end re-read a clamped pixel):
     // a predicated load would make the ring slot a phi and force an early wait.
@@ -246,7 +303,19 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     o[i] = (float)((double)o[i] + (du_first ? c : c + 0.0));
                 }
             }
-            if (k < g.n) {
+            if (WTA) {
+                // lane-local first-min over this lane's disparities, parked in LDS; the 64-way
+                // merge runs once per PF steps (below), off the recurrence's serial chain
+                float bv = __builtin_inff();
+                int ba = 0x7fffffff;
+#pragma unroll
+                for (int i = 0; i < DPL; i++)
+                    if (dbase + i < D && o[i] < bv) { bv = o[i]; ba = dbase + i; }
+                if (lane == 0 && o[0] != o[0]) { bv = -__builtin_inff(); ba = 0; }   // NaN S(0): d = 0
+                wbv[j * 64 + lane] = bv;
+                wba[j * 64 + lane] = ba;
+                if (lane == 0) wpx[j] = k < g.n ? (int)(sl.off / D) : -1;
+            } else if (k < g.n) {
                 if (VEC) {
                     if (dbase < D) {
                         FVec<DPL> ov;
@@ -271,6 +340,36 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
             ahead.advance(g);
         }
+        if (WTA) {
+            // PF pixels x 64 lane partials: lane l merges lanes 8(l&7)..+7 of step l>>3 (increasing
+            // d), then the 8 octants of its step by xor-butterfly; the merge is a total order
+            // (first-min with index tie-break, no NaN partials), so any merge order agrees
+            constexpr int G = 64 / PF;      // lanes per step; each merges PF partials
+            const int st = lane / G, q = lane % G;
+            float bv = wbv[st * 64 + PF * q];
+            int ba = wba[st * 64 + PF * q];
+#pragma unroll
+            for (int t = 1; t < PF; t++) wta_merge(bv, ba, wbv[st * 64 + PF * q + t], wba[st * 64 + PF * q + t]);
+#pragma unroll
+            for (int o2 = 1; o2 < G; o2 <<= 1) wta_merge(bv, ba, __shfl_xor(bv, o2, 64), __shfl_xor(ba, o2, 64));
+            const int px = wpx[st];
+            if (q == 0 && px >= 0) sd.disp[px] = (float)(ba == 0x7fffffff ? 0 : ba);
+        }
+    }
+    if (WTA && g.n < nlen) {
+        // pixels of this line's direction never visited: the last line position's successor.
+        // DU-RL (the reference's last direction) walks rows H-1 .. 1 and never reaches row 0:
+        // pixel (0, line) is one of them for every line; other directions map analogously.
+        int r0, c0;
+        if (g.dc == 0) { r0 = g.dr > 0 ? H - 1 : 0; c0 = line; }
+        else if (g.dr == 0) { r0 = line; c0 = g.dc > 0 ? W - 1 : 0; }
+        else { r0 = g.dr > 0 ? H - 1 : 0; c0 = line; }
+        const size_t off = ((size_t)r0 * W + c0) * D;
+        float o[DPL];
+#pragma unroll
+        for (int i = 0; i < DPL; i++) o[i] = sd.S[off + min(dbase + i, D - 1)];
+        const int a = wta_pixel<DPL>(o, dbase, D);
+        if (lane == 63) sd.disp[off / D] = (float)a;
     }
     if (FIRST || DU) {
         // rows UD never visits (it stops at row n-1): S := 0 (FIRST), then DU's term
@@ -292,51 +391,56 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     }
 }
 
-template <int DPL, bool VEC, bool FIRST, bool DU>
+template <int DPL, bool VEC, bool FIRST, bool DU, bool WTA>
 static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
                         hipStream_t st)
 {
     const bool horiz = (dir == 2 || dir == 3);
     const int nlines = horiz ? H : W;
     constexpr int PF = DPL <= 4 ? 8 : 4;
-    sgm_scan_kernel<DPL, PF, VEC, FIRST, DU><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
+    sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
 }
 
+// mode: 0 accumulate, 1 first (S := 0 + L), 2 first + DU fold, 3 accumulate + DU fold,
+// 4 accumulate + fused WTA (the last direction)
 template <int DPL, bool VEC>
-static void launch_mode(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, bool first,
-                        bool du, hipStream_t st)
+static void launch_mode(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, int mode,
+                        hipStream_t st)
 {
-    if (first) {
-        if (du) launch_scan<DPL, VEC, true, true>(a, b, nsides, H, W, D, dir, st);
-        else launch_scan<DPL, VEC, true, false>(a, b, nsides, H, W, D, dir, st);
-    } else {
-        if (du) launch_scan<DPL, VEC, false, true>(a, b, nsides, H, W, D, dir, st);
-        else launch_scan<DPL, VEC, false, false>(a, b, nsides, H, W, D, dir, st);
+    switch (mode) {
+    case 1: launch_scan<DPL, VEC, true, false, false>(a, b, nsides, H, W, D, dir, st); break;
+    case 2: launch_scan<DPL, VEC, true, true, false>(a, b, nsides, H, W, D, dir, st); break;
+    case 3: launch_scan<DPL, VEC, false, true, false>(a, b, nsides, H, W, D, dir, st); break;
+    case 4: launch_scan<DPL, VEC, false, false, true>(a, b, nsides, H, W, D, dir, st); break;
+    default: launch_scan<DPL, VEC, false, false, false>(a, b, nsides, H, W, D, dir, st); break;
     }
 }
 
 template <int DPL>
-static void launch_dpl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, bool first,
-                       bool du, hipStream_t st)
+static void launch_dpl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, int mode,
+                       hipStream_t st)
 {
-    if ((D % DPL) == 0) launch_mode<DPL, true>(a, b, nsides, H, W, D, dir, first, du, st);
-    else launch_mode<DPL, false>(a, b, nsides, H, W, D, dir, first, du, st);
+    if ((D % DPL) == 0) launch_mode<DPL, true>(a, b, nsides, H, W, D, dir, mode, st);
+    else launch_mode<DPL, false>(a, b, nsides, H, W, D, dir, mode, st);
 }
 
 // One direction over one or two sides; first: S := f32(0 + L) (no S read); du (dir 0
-// only): direction DU folded into the same pass (see sgm_scan_kernel).
+// only): direction DU folded into the same pass; wta: the final S is reduced to the
+// disparity map (sd.disp) instead of being stored (see sgm_scan_kernel).
 static int sgm_direction_impl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
-                              bool first, hipStream_t st, bool du = false)
+                              bool first, hipStream_t st, bool du = false, bool wta = false)
 {
+    const int mode = wta ? 4 : (first ? (du ? 2 : 1) : (du ? 3 : 0));
+    if (wta && (first || du)) return SDE_ERR_ARG;
     switch ((D + 63) / 64) {
-    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, first, du, st); break;
-    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, first, du, st); break;
+    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, mode, st); break;
     default: return SDE_ERR_ARG;
     }
     return SDE_OK;
@@ -550,7 +654,7 @@ SDE_EXPORT int sde_sgm_direction(const float *cv, const float *pen, int H, int W
 {
     if (!cv || !pen || !S || H < 2 || W < 2 || D <= 0 || D > 512 || direction < 0 || direction > 7)
         return SDE_ERR_ARG;
-    const SgmSide a{cv, pen, S};
+    const SgmSide a{cv, pen, S, nullptr};
     const int s = sgm_direction_impl(a, a, 1, H, W, D, direction, false, as_stream(stream));
     if (s != SDE_OK) return s;
     return launch_status();
@@ -561,25 +665,40 @@ SDE_EXPORT int sde_sgm_8path(const float *cv, const float *pen, int H, int W, in
     return sde_sgm_8path_pair(cv, pen, S, nullptr, nullptr, nullptr, H, W, D, SDE_SGM_ACCUMULATE, stream);
 }
 
-SDE_EXPORT int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r,
-                                  const float *pen_r, float *S_r, int H, int W, int D, int flags, void *stream)
+static int sgm_pair(const float *cv_l, const float *pen_l, float *S_l, float *disp_l, const float *cv_r,
+                    const float *pen_r, float *S_r, float *disp_r, int H, int W, int D, int flags, bool wta,
+                    hipStream_t st)
 {
     if (!cv_l || !pen_l || !S_l || H < 2 || W < 2 || D <= 0 || D > 512 ||
         (flags & ~(SDE_SGM_ACCUMULATE | SDE_SGM_ZERO_DU_PENALTIES)))
         return SDE_ERR_ARG;
     const bool two = cv_r || pen_r || S_r;
     if (two && (!cv_r || !pen_r || !S_r)) return SDE_ERR_ARG;
-    const SgmSide a{cv_l, pen_l, S_l};
-    const SgmSide b = two ? SgmSide{cv_r, pen_r, S_r} : a;
+    if (wta && (!disp_l || (two && !disp_r))) return SDE_ERR_ARG;
+    const SgmSide a{cv_l, pen_l, S_l, disp_l};
+    const SgmSide b = two ? SgmSide{cv_r, pen_r, S_r, disp_r} : a;
     const bool fold_du = (flags & SDE_SGM_ZERO_DU_PENALTIES) != 0;
     for (int dir = 0; dir < 8; dir++) {
         if (dir == 1 && fold_du) continue;                               // applied in the UD pass
         const bool first = dir == 0 && !(flags & SDE_SGM_ACCUMULATE);   // UD: line = column
-        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, as_stream(stream),
-                                         dir == 0 && fold_du);
+        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, st, dir == 0 && fold_du,
+                                         wta && dir == 7);
         if (s != SDE_OK) return s;
     }
     return launch_status();
+}
+
+SDE_EXPORT int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r,
+                                  const float *pen_r, float *S_r, int H, int W, int D, int flags, void *stream)
+{
+    return sgm_pair(cv_l, pen_l, S_l, nullptr, cv_r, pen_r, S_r, nullptr, H, W, D, flags, false, as_stream(stream));
+}
+
+SDE_EXPORT int sde_sgm_8path_wta_pair(const float *cv_l, const float *pen_l, float *S_l, float *disp_l,
+                                      const float *cv_r, const float *pen_r, float *S_r, float *disp_r, int H, int W,
+                                      int D, int flags, void *stream)
+{
+    return sgm_pair(cv_l, pen_l, S_l, disp_l, cv_r, pen_r, S_r, disp_r, H, W, D, flags, true, as_stream(stream));
 }
 
 SDE_EXPORT int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,

@@ -356,6 +356,28 @@ def sgm_8path_pair(cv_l, pen_l, S_l, cv_r=None, pen_r=None, S_r=None, accumulate
     return S_l, S_r
 
 
+def sgm_8path_wta_pair(cv_l, pen_l, S_l, disp_l=None, cv_r=None, pen_r=None, S_r=None, disp_r=None,
+                       accumulate=False, zero_du_penalties=False):
+    """sgm_8path_pair + WTA (rule "d0") fused into the last direction (sde_sgm_8path_wta_pair):
+    returns the disparity maps; S is left holding the first seven directions' sum."""
+    H, W, D = cv_l.shape
+    if disp_l is None:
+        disp_l = _empty((H, W), torch.float32, cv_l)
+    args = [_need(cv_l, "cost volume"), _need(pen_l, "penalties", shape=(H, W, 16)), _need(S_l, "S", shape=(H, W, D)),
+            _need(disp_l, "disp", shape=(H, W))]
+    if cv_r is None:
+        args += [None, None, None, None]
+    else:
+        if disp_r is None:
+            disp_r = _empty((H, W), torch.float32, cv_l)
+        args += [_need(cv_r, "cost volume", shape=(H, W, D)), _need(pen_r, "penalties", shape=(H, W, 16)),
+                 _need(S_r, "S", shape=(H, W, D)), _need(disp_r, "disp", shape=(H, W))]
+    flags = (_lib.SDE_SGM_ACCUMULATE if accumulate else 0) | \
+        (_lib.SDE_SGM_ZERO_DU_PENALTIES if zero_du_penalties else 0)
+    check(lib.sde_sgm_8path_wta_pair(*args, H, W, D, flags, _stream()), "sde_sgm_8path_wta_pair")
+    return disp_l, disp_r
+
+
 def sgm_direction(cv_hwd, pen, direction: int, S):
     H, W, D = cv_hwd.shape
     check(lib.sde_sgm_direction(_need(cv_hwd, "cost volume"), _need(pen, "penalties", shape=(H, W, 16)), H, W, D,

@@ -170,13 +170,11 @@ class StereoMatcher:
         ops.sgm_penalties(img_l, out=b["pen"][0])
         ops.sgm_penalties(img_r, out=b["pen"][1])
         # both sides per launch (the reference's k loop); S := 8-path sum, no zero-fill pass
-        # penalties from sgm_penalties (channels 0/1 zero), finite costs: DU folds into UD
-        ops.sgm_8path_pair(b["cv"][0], b["pen"][0], b["S"][0], b["cv"][1], b["pen"][1], b["S"][1],
-                           zero_du_penalties=True)
+        # penalties from sgm_penalties (channels 0/1 zero), finite costs: DU folds into UD;
+        # WTA_and_SupixelRefinement_kernel (:800-837) fused into the last direction
+        ops.sgm_8path_wta_pair(b["cv"][0], b["pen"][0], b["S"][0], b["disp"][0], b["cv"][1], b["pen"][1],
+                               b["S"][1], b["disp"][1], zero_du_penalties=True)
         t = mark("sgm", t)
-        for k in range(2):
-            ops.wta(b["S"][k], layout="HWD", rule="d0", out=b["disp"][k])
-        t = mark("wta", t)
         if not post:
             return b["disp"][0], b["disp"][1]
         b["lrc"][0].zero_()

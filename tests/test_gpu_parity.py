@@ -312,6 +312,36 @@ def test_cbca_bit_exact(gpu, oracle, H, W, D, L1, iters, side):
     assert host(got).tobytes() == want.tobytes()
 
 
+@pytest.mark.parametrize("H,W,D", [(33, 70, 97), (19, 41, 192), (5, 130, 64), (70, 9, 300), (2, 50, 64),
+                                   (3, 2, 16), (2, 2, 4), (40, 33, 128)])
+def test_sgm_8path_wta_pair_bit_exact(gpu, oracle, H, W, D):
+    """WTA fused into the last direction == sgm_8path followed by the reference's WTA rule, both
+    sides, with NaN / +inf / tie patterns in the final S (first-min and the d = 0 rule)."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(3 * H + W + D)
+    cvs, pens, wants = [], [], []
+    for k in range(2):
+        cv = (rng.standard_normal((H, W, D)) * 0.5).astype(np.float32)
+        cv[rng.random((H, W, D)) < 0.1] = 1.0
+        cv[0, 0, :] = 0.25                      # a pixel whose costs tie at every d
+        pen = oracle.sgm_penalties(rng.integers(0, 256, (H, W)).astype(np.uint8))
+        ref = oracle.sgm_8path(cv, pen)
+        cvs.append(cv), pens.append(pen), wants.append(oracle.wta_sgm(ref))
+    for fold in (False, True):
+        S = [torch.full((H, W, D), float("nan"), device="cuda") for _ in range(2)]
+        dl, dr = ops.sgm_8path_wta_pair(dev(cvs[0]), dev(pens[0]), S[0], None, dev(cvs[1]), dev(pens[1]), S[1],
+                                        None, zero_du_penalties=fold)
+        assert np.array_equal(host(dl), wants[0]), fold
+        assert np.array_equal(host(dr), wants[1]), fold
+    # one side, accumulate mode onto an S with NaN / inf entries
+    S0 = rng.standard_normal((H, W, D)).astype(np.float32)
+    S0[rng.random((H, W, D)) < 0.02] = np.inf
+    S0[0, :, 0] = np.nan
+    want = oracle.wta_sgm(oracle.sgm_8path(cvs[0], pens[0], S0.copy()))
+    d1, _ = ops.sgm_8path_wta_pair(dev(cvs[0]), dev(pens[0]), dev(S0), accumulate=True)
+    assert np.array_equal(host(d1), want)
+
+
 def test_matcher_cbca_sgm_end_to_end(gpu, oracle):
     """StereoMatcher.sgm_path with CBCA before SGM == the oracle composition on the same inputs."""
     from scenedepthestimation_amd.pipeline import StereoMatcher
