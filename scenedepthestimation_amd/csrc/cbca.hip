@@ -47,6 +47,18 @@ __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict_
     arms[p] = packed;
 }
 
+// Buffer descriptor (wave-uniform inputs only) for raw dword loads/stores with a 32-bit
+// per-lane voffset, an SGPR soffset and the hardware range check (voffset >= bytes -> 0 on
+// load, dropped on store).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cb_rsrc(const void *base, uint32_t bytes)
+{
+    const uintptr_t b = (uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    void *p = (void *)(((uintptr_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 template <int R, bool VERT, int SIDE>
 __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__ src, float *__restrict__ dst,
                                                        const uint32_t *__restrict__ ref,
@@ -64,50 +76,53 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     const int d = min((int)blockIdx.x * 64 + lane, D - 1);
     const int line = blockIdx.y;
     const int len = VERT ? H : W;
-    // opaque per-lane zero: keeps the (wave-uniform) reference-arm load a vector load,
-    // ordered under vmcnt with the rest of the ring instead of a scalar load whose
-    // out-of-order lgkmcnt (shared with the LDS ring) would serialise every step
-    const int vz = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    // per-position strides (elements) and per-line bases: position q of this line is
-    // src/dst + cbase + q*cstride, ref + abase + q*astride, oth + abase + q*astride + o(q)
-    const int cstride = VERT ? W * D : D, astride = VERT ? W : 1;
-    const size_t cbase = VERT ? (size_t)line * D : (size_t)line * W * D;
-    const size_t abase = VERT ? (size_t)line : (size_t)line * W;
-    // vertical pass: the other pixel (line -/+ d) is fixed for the whole column
+    // Addressing (all per-step offsets in SGPRs, per-lane parts fixed):
+    //  H pass (line = row y): cost/out buffers over the row, voffset 4d, soffset 4qD; reference
+    //   arms: voffset 0, soffset 4q; other arms: voffset 4(q -/+ d) -- outside the row it fails
+    //   the range check and reads 0, i.e. "no other pixel: support {p}".
+    //  V pass (line = column x): cost/out buffers rebased every RS rows (a column spans
+    //   H*W*D*4 bytes, beyond 32-bit offsets), voffset 4d, soffset 4(q - q0)WD; arms: voffset 0 /
+    //   4(x -/+ d) (masked when outside the row), soffset 4qW.
+    const uint32_t d4 = 4u * d;
+    // opaque per-lane zero for the (wave-uniform) reference-arm loads: keeps their value a VGPR,
+    // so no readfirstlane (and no wait for it) lands on every step
+    const uint32_t vz = __builtin_amdgcn_mbcnt_lo(0u, 0u);
     const int ov = SIDE == SDE_SIDE_LEFT ? line - d : line + d;
     const bool vok = ov >= 0 && ov < W;
-    const int ovc = (vok ? ov : 0) - line;          // offset from the reference pixel
+    const uint32_t ov4 = 4u * (uint32_t)(vok ? ov : 0);
+    const uint32_t linebytes = 4u * (uint32_t)W * (uint32_t)D;       // one row of the volume
+    __amdgpu_buffer_rsrc_t rc, rd;
+    __amdgpu_buffer_rsrc_t ra = cb_rsrc(ref + (VERT ? (size_t)line : (size_t)line * W), VERT ? 0xffffffffu : 4u * W);
+    __amdgpu_buffer_rsrc_t rb = cb_rsrc(oth + (VERT ? 0 : (size_t)line * W), VERT ? 0xffffffffu : 4u * W);
+    if (!VERT) {
+        rc = cb_rsrc(src + (size_t)line * W * D, linebytes);
+        rd = cb_rsrc(dst + (size_t)line * W * D, linebytes);
+    }
 
     double P_acc = 0.0;
     int N_acc = 0;
     float cr[PF];
     uint32_t ar[PF], br[PF];
     uint32_t sup[U];    // VERT: (up | down << 8) of the last U positions; else (left | right << 8)
-    auto issue = [&](int q, int slot) {
-        const float *pc = src + cbase + (size_t)q * cstride;
-        const uint32_t *pa = ref + abase + (size_t)q * astride;
-        cr[slot] = pc[d];
-        ar[slot] = pa[vz];
-        int oo;
+    // q: position (clamped by the caller in the tail); qb: the V pass's current rebase row
+    auto issue = [&](int q, int qb, int slot) {
         if (VERT) {
-            oo = ovc;
+            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rc, d4, (int)((uint32_t)(q - qb) * linebytes), 0));
+            ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q * W, 0);
+            br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, ov4, 4 * q * W, 0);
         } else {
-            const int o = SIDE == SDE_SIDE_LEFT ? q - d : q + d;
-            oo = (o < 0 ? 0 : (o >= W ? W - 1 : o)) - q;
+            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, d4, 4 * q * D, 0));
+            ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q, 0);
+            const uint32_t o4 = SIDE == SDE_SIDE_LEFT ? 4u * (uint32_t)q - d4 : 4u * (uint32_t)q + d4;
+            br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, o4, 0, 0);
         }
-        br[slot] = pa[oo + (oth - ref)];
     };
-    auto step = [&](int j, int f, bool tail) {
+    auto step = [&](int j, int f, int qb, bool tail) {
         const int slot = j % PF;
         const uint32_t a = ar[slot];
         uint32_t b = br[slot];
-        if (VERT) {
-            b = vok ? b : 0u;                       // no other pixel: support {p}
-        } else {
-            const int x = tail ? (f < len ? f : len - 1) : f;
-            const bool ok = SIDE == SDE_SIDE_LEFT ? d <= x : d < W - x;
-            b = ok ? b : 0u;
-        }
+        if (VERT) b = vok ? b : 0u;                 // no other pixel: support {p}
         const int l = min(a & 255, b & 255), r = min((a >> 8) & 255, (b >> 8) & 255);
         // front: position f (tail positions >= len re-read the last one; never referenced)
         P_acc += (double)cr[slot];
@@ -119,7 +134,8 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
         } else {
             sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
         }
-        issue(tail ? min(f + PF, len - 1) : f + PF, slot);
+        const int qn = tail ? min(f + PF, len - 1) : f + PF;
+        issue(qn, qb, slot);
         // trailing output y = f - R; its support arms from the ring slot of position y
         const int y = f - R;
         if (y >= 0 && (!tail || y < len)) {
@@ -130,11 +146,25 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
             float out;
             if (VERT) out = (float)((pb - pa) / (double)(sN[ib] - sN[ia]));
             else out = (float)(pb - pa);
-            (dst + cbase + (size_t)y * cstride)[d] = out;
+            const int so = VERT ? (int)((uint32_t)(y - qb) * linebytes) : 4 * y * D;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, d4, so, 0);
         }
     };
+    // V pass: (re)base the cost / output descriptors on row qb; soffsets then stay below
+    // (2 RS + PF) rows of the volume
+    auto rebase = [&](int qb) {
+        if (VERT) {
+            const size_t off = (size_t)qb * W * D + (size_t)line * D;
+            rc = cb_rsrc(src + off, 0xffffffffu);
+            rd = cb_rsrc(dst + off, 0xffffffffu);
+        }
+    };
+    // V pass: the descriptors are rebased on row qb = f0 - R at every block start, so a block's
+    // outputs (rows f0 - R ..) and loads (rows up to f0 + RS + PF) sit at small soffsets; loads
+    // already in flight keep the addresses they were issued with.
+    rebase(-R);
 #pragma unroll
-    for (int j = 0; j < PF; j++) issue(min(j, len - 1), j);
+    for (int j = 0; j < PF; j++) issue(min(j, len - 1), -R, j);
 #pragma unroll
     for (int j = 0; j < U; j++) sup[j] = 0u;
     sP[(RS - 1) * 64 + lane] = 0.0;        // P(-1) = 0 (slot of position -1; rewritten at f = RS-1)
@@ -142,12 +172,16 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     int f0 = 0;
     // main blocks: every prefetched position is inside the line (no clamps)
     for (; f0 + RS + PF <= len; f0 += RS) {
+        const int qb = f0 - R;
+        rebase(qb);
 #pragma unroll
-        for (int j = 0; j < RS; j++) step(j, f0 + j, false);
+        for (int j = 0; j < RS; j++) step(j, f0 + j, qb, false);
     }
     for (; f0 < len + R; f0 += RS) {
+        const int qb = f0 - R;
+        rebase(qb);
 #pragma unroll
-        for (int j = 0; j < RS; j++) step(j, f0 + j, true);
+        for (int j = 0; j < RS; j++) step(j, f0 + j, qb, true);
     }
 }
 
