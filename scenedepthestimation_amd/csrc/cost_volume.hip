@@ -34,14 +34,20 @@ constexpr int CV_ROWS = CV_TX + CV_DC - 1;   // other-side rows per chunk
 
 enum { OUT_WTA = 0, OUT_DHW = 1, OUT_HWD = 2, OUT_HWD_LR = 3 };
 
-// Exact -(0 + pairwise8) of own[64] (registers) and one swizzled LDS row.
+// LDS image of the "other" rows: 64 floats + one 16-B pad per row (272 B), so the lanes of a
+// ds_read_b128 group, which read the same chunk of consecutive rows, start 4 banks apart
+// (conflict-free) and every chunk address is the row base plus an immediate offset.
+constexpr int CV_RSTRIDE = 17;     // float4 per LDS row
+
+// Exact -(0 + pairwise8) of own[64] (registers) and one padded LDS row.
 __device__ __forceinline__ float dot64_exact(const float (&own)[64], const float4 *__restrict__ win, int lr)
 {
     float acc[8];
+    const float4 *row = win + lr * CV_RSTRIDE;
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-        const float4 a = win[swz_row16(lr, 2 * m)];
-        const float4 b = win[swz_row16(lr, 2 * m + 1)];
+        const float4 a = row[2 * m];
+        const float4 b = row[2 * m + 1];
         const float p0 = own[8 * m + 0] * a.x, p1 = own[8 * m + 1] * a.y;
         const float p2 = own[8 * m + 2] * a.z, p3 = own[8 * m + 3] * a.w;
         const float p4 = own[8 * m + 4] * b.x, p5 = own[8 * m + 5] * b.y;
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
                                                    float *__restrict__ out_r)
 {
     constexpr bool TILE = OUT == OUT_HWD || OUT == OUT_HWD_LR;
-    __shared__ float4 win[CV_ROWS * 16];
+    __shared__ float4 win[CV_ROWS * CV_RSTRIDE];
     __shared__ float otile[TILE ? CV_TX * (CV_DC + 1) : 1];
 
     const int lane = threadIdx.x & 63;
@@ -103,11 +109,12 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
         __syncthreads();   // previous chunk's LDS reads (win and otile) are complete
         for (int idx = threadIdx.x; idx < CV_ROWS * 16; idx += 256) {
             const int lr = idx >> 4, k = idx & 15, g = rbase + lr;
-            if (g >= 0 && g < W) win[swz_row16(lr, k)] = other4[(size_t)g * 16 + k];
+            if (g >= 0 && g < W) win[lr * CV_RSTRIDE + k] = other4[(size_t)g * 16 + k];
         }
         __syncthreads();
         const int ds = dc + wave * CV_DW;
         const int de = min(ds + CV_DW, dce);
+#pragma unroll 2
         for (int d = ds; d < de; d++) {
             const int o = (SIDE == SDE_SIDE_LEFT) ? q - d : q + d;
             const bool valid = (SIDE == SDE_SIDE_LEFT) ? (o >= 0) : (o < W);
