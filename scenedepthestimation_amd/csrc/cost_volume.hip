@@ -15,10 +15,11 @@
 // Mapping (C = 64 fast path): a workgroup is 4 waves on one image row and 64
 // consecutive "own" pixels (one per lane, its 64-float feature vector held in
 // VGPRs).  The 127 "other" feature rows a 64-disparity chunk touches are staged
-// in LDS (XOR-swizzled 256-B rows: the 16 lanes of a ds_read_b128 group read 16
+// in LDS (272-B padded rows: the 16 lanes of a ds_read_b128 group read 16
 // consecutive rows -> 16 distinct bank slots).  Wave w sweeps disparities
 // [16w, 16w+16) of each chunk; the fused WTA merges the 4 per-wave first-minima
-// by (value, index) at the end, which equals the sequential scan.
+// by (value, index) at the end, which equals the sequential scan.  The GPU
+// path's L and R volumes come from one row sweep (cvlr_row_kernel, below).
 #include "sde_common.h"
 #include "cv_cert.h"
 
@@ -32,7 +33,7 @@ constexpr int CV_DC = 64;                    // disparities per LDS chunk
 constexpr int CV_DW = CV_DC / CV_WAVES;      // disparities per wave per chunk
 constexpr int CV_ROWS = CV_TX + CV_DC - 1;   // other-side rows per chunk
 
-enum { OUT_WTA = 0, OUT_DHW = 1, OUT_HWD = 2, OUT_HWD_LR = 3 };
+enum { OUT_WTA = 0, OUT_DHW = 1, OUT_HWD = 2 };
 
 // LDS image of the "other" rows: 64 floats + one 16-B pad per row (272 B), so the lanes of a
 // ds_read_b128 group, which read the same chunk of consecutive rows, start 4 banks apart
@@ -66,19 +67,14 @@ __device__ __forceinline__ float dot64_exact(const float (&own)[64], const float
 
 // SIDE_LEFT : own = fl at x,  other = fr at x - d   (L[y][x][d])
 // SIDE_RIGHT: own = fr at x', other = fl at x' + d  (R[y][x'][d] = cost(x'+d, d))
-// OUT_HWD_LR (SIDE_LEFT only): every voxel is computed once and stored twice,
-// L[y][q][d] and R[y][q-d][d] (the right volume is the left one sheared, bit for bit:
-// the products commute and the channel order is the same).  The grid runs D-1 pixels
-// past the row end so the blocks owning q >= W write R's invalid fill.
 template <int SIDE, int OUT>
 __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own_feat,
                                                    const float *__restrict__ other_feat, int H, int W,
                                                    int d0, int d1, int Dvol, float invalid,
                                                    float *__restrict__ out, float *__restrict__ out_min,
-                                                   int32_t *__restrict__ out_arg, float *__restrict__ out_disp,
-                                                   float *__restrict__ out_r)
+                                                   int32_t *__restrict__ out_arg, float *__restrict__ out_disp)
 {
-    constexpr bool TILE = OUT == OUT_HWD || OUT == OUT_HWD_LR;
+    constexpr bool TILE = OUT == OUT_HWD;
     __shared__ float4 win[CV_ROWS * CV_RSTRIDE];
     __shared__ float otile[TILE ? CV_TX * (CV_DC + 1) : 1];
 
@@ -136,16 +132,6 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
                     out[((size_t)y * W + q0 + i) * Dvol + dc + lane] = otile[i * (CV_DC + 1) + lane];
             }
         }
-        if (OUT == OUT_HWD_LR) {
-            // R band of this tile: x' = q0 - dc - 63 + t, lane = d - dc, own pixel ql = lane + t - 63
-            const int nd = dce - dc;
-            for (int t = wave; t < 2 * CV_TX - 1; t += CV_WAVES) {
-                const int xr = q0 - dc - (CV_TX - 1) + t;
-                const int ql = lane + t - (CV_TX - 1);
-                if (xr >= 0 && xr < W && ql >= 0 && ql < CV_TX && lane < nd)
-                    out_r[((size_t)y * W + xr) * Dvol + dc + lane] = otile[ql * (CV_DC + 1) + lane];
-            }
-        }
     }
 
     if (OUT == OUT_WTA) {
@@ -161,6 +147,190 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
             if (out_min) out_min[p] = best;
             if (out_arg) out_arg[p] = arg;
             if (out_disp) out_disp[p] = (float)arg;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// L and R volumes in one row sweep (C = 64, [H,W,D]).
+//
+// A workgroup owns one image row y and one 64-disparity chunk [dc, dc+nd) and
+// sweeps the row in 64-pixel strips q0 = 0, 64, ...  Lane (p, h) = (lane&31,
+// lane>>5) of wave w holds TWO adjacent own pixels u = q0+2p, u+1 in VGPRs and
+// the 8 disparities e..e+7 (e = dc + 16w + 8h): rows o = u+1-e-j, j = 0..8,
+// serve both pixels (pixel u+1 at d = e+j, pixel u at d = e+j-1), so 9 LDS row
+// reads feed 16 dots -- 144 B of LDS per voxel instead of 256.
+//   * other-side rows: a 128-row LDS ring of 272-B rows; a strip needs rows
+//     [q0-dc-63, q0-dc+63] and stages only its 64 new ones.  Ring slot of row
+//     x = g&127 is (x>>1) | (x&1)<<6, so the even (or odd) rows one ds_read_b128
+//     group reads land in 16 distinct 16-B bank slots with immediate offsets;
+//   * every voxel lands in a 128-row LDS ring of R rows, R[y][q-d][d] (the right
+//     volume is the left one sheared, bit for bit); a strip emits the 64 R rows
+//     it completed as full runs (lane = disparity).  Columns are XOR-swizzled by
+//     (row>>1)&31 so the 32 rows a ds_write_b32 half-wave hits use 32 banks;
+//   * the strip's own pixels are staged (coalesced) into the half of the R ring
+//     that this strip writes last, and copied to VGPRs before it does;
+//   * L[y][q][d] leaves straight from registers (32-B pieces of the runs);
+//   * a strip's global loads are issued right after the previous strip's dot
+//     loop and L stores, into registers, so their latency overlaps the R
+//     emission and the barriers.
+// Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
+// ---------------------------------------------------------------------------
+#ifndef CVLR_SKIP
+#define CVLR_SKIP 0   // profiling builds only (tools/cvlr_variants.sh): 1 L stores, 2 R stores, 4 dots, 8 loads
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr size_t CVR_RING_BYTES = (size_t)128 * CV_RSTRIDE * 16;     // other-side rows
+constexpr size_t CVR_SMEM = CVR_RING_BYTES + (size_t)128 * 64 * 4;    // + R ring
+
+__device__ __forceinline__ int cvr_slot(int g) { const int x = g & 127; return (x >> 1) | ((x & 1) << 6); }
+__device__ __forceinline__ int cvr_rword(int xr, int col) { return (xr & 127) * 64 + (col ^ ((xr >> 1) & 31)); }
+
+__global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restrict__ fl,
+                                                          const float *__restrict__ fr, int H, int W, int D,
+                                                          int nchunks, float invalid, float *__restrict__ outl,
+                                                          float *__restrict__ outr)
+{
+    extern __shared__ f32x4 cvr_sm[];
+    f32x4 *ring = cvr_sm;                                                         // 128 x 17 f32x4
+    float *rring = reinterpret_cast<float *>(reinterpret_cast<char *>(cvr_sm) + CVR_RING_BYTES);  // 128 x 64
+
+    const int job = xcd_remap(blockIdx.x, gridDim.x);   // the chunks of a row share an XCD's L2
+    const int y = job / nchunks;
+    const int dc = (job - y * nchunks) * CV_DC;
+    const int nd = min(CV_DC, D - dc);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = lane & 31, h = lane >> 5;
+    const int e = dc + 16 * wave + 8 * h;               // this lane's first disparity
+    const bool active = e < dc + nd;                    // uniform per half-wave
+    const size_t rowvox = (size_t)y * W;
+    const f32x4 *fl4 = reinterpret_cast<const f32x4 *>(fl) + rowvox * 16;
+    const f32x4 *fr4 = reinterpret_cast<const f32x4 *>(fr) + rowvox * 16;
+    const bool vec = (D & 3) == 0 && e + 8 <= dc + nd;
+
+    const int nstrips = (W - 1 + dc + CV_TX - 1) / CV_TX + 1;   // the last strip emits R row W-1
+    f32x4 sfr[4], sown[4];
+    auto load_strip = [&](int q0) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int idx = threadIdx.x + 256 * i, c = idx & 15;
+            const int g = q0 - dc + (idx >> 4), x = q0 + (idx >> 4);
+            if (!(CVLR_SKIP & 8) && g >= 0 && g < W) sfr[i] = fr4[(size_t)g * 16 + c];
+            if (!(CVLR_SKIP & 8) && x < W) sown[i] = fl4[(size_t)x * 16 + c];
+        }
+    };
+    load_strip(0);
+    for (int k = 0; k < nstrips; k++) {
+        const int q0 = k * CV_TX;
+        // the R-ring half of rows [q0-dc, q0-dc+63]: unwritten until this strip's dot loop
+        f32x4 *ownbuf = reinterpret_cast<f32x4 *>(rring + (((q0 - dc) & 127) >> 6) * 64 * 64);
+        // [A] other-side rows [q0-dc, q0-dc+63] -> ring, own pixels [q0, q0+63] -> ownbuf
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int idx = threadIdx.x + 256 * i, c = idx & 15;
+            const int g = q0 - dc + (idx >> 4), x = q0 + (idx >> 4);
+            if (!(CVLR_SKIP & 8) && g >= 0 && g < W) ring[cvr_slot(g) * CV_RSTRIDE + c] = sfr[i];
+            if (!(CVLR_SKIP & 8) && x < W) ownbuf[(x & 63) * 16 + (c ^ ((x >> 1) & 15))] = sown[i];
+        }
+        const int u = q0 + 2 * p;
+        const bool compute = q0 < W;
+        __syncthreads();
+        // channel pairs as 2-vectors: the products and running sums are v_pk_mul_f32 /
+        // v_pk_add_f32 on aligned register pairs (each lane still rounds exactly as the scalar code)
+        f32x2 own_a[32], own_b[32];
+        if (active && compute) {
+            const f32x4 *sa = ownbuf + (u & 63) * 16, *sb = sa + 16;
+            const int sw = (u >> 1) & 15;                  // pixels u and u+1 share it
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const f32x4 va = sa[c ^ sw], vb = sb[c ^ sw];
+                own_a[2 * c] = va.xy; own_a[2 * c + 1] = va.zw;
+                own_b[2 * c] = vb.xy; own_b[2 * c + 1] = vb.zw;
+            }
+        }
+        __syncthreads();                                    // ownbuf is R-ring space again
+        // [B] 9 rows x 2 pixels; every cost goes to registers (L) and the R ring
+        const bool aok = u < W, bok = u + 1 < W;
+        const int obase = u + 1 - e;
+        float ca[8], cb[8];
+        if (active) {
+            if (compute && !(CVLR_SKIP & 4)) {
+#pragma unroll
+                for (int j = 0; j < 9; j++) {
+                    const int o = obase - j;
+                    const f32x4 *row = ring + cvr_slot(o) * CV_RSTRIDE;
+                    f32x2 xa[4], xb[4];     // accumulators (0,1) (2,3) (4,5) (6,7)
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        const f32x4 a = row[2 * m], b = row[2 * m + 1];
+                        const f32x2 r[4] = {a.xy, a.zw, b.xy, b.zw};
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            if (j <= 7) {
+                                const f32x2 pr = own_b[4 * m + t] * r[t];
+                                xb[t] = m == 0 ? pr : xb[t] + pr;
+                            }
+                            if (j >= 1) {
+                                const f32x2 pr = own_a[4 * m + t] * r[t];
+                                xa[t] = m == 0 ? pr : xa[t] + pr;
+                            }
+                        }
+                    }
+                    if (j <= 7) {
+                        const float s = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
+                                        ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
+                        cb[j] = (bok && o >= 0) ? -(0.0f + s) : invalid;
+                        rring[cvr_rword(o, e - dc + j)] = cb[j];
+                    }
+                    if (j >= 1) {
+                        const float s = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
+                                        ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
+                        ca[j - 1] = (aok && o >= 0) ? -(0.0f + s) : invalid;
+                        rring[cvr_rword(o, e - dc + j - 1)] = ca[j - 1];
+                    }
+                }
+            } else {
+                // past the row end: R's invalid fill only
+#pragma unroll
+                for (int j = 0; j < 9; j++) {
+                    if (j <= 7) rring[cvr_rword(obase - j, e - dc + j)] = invalid;
+                    if (j >= 1) rring[cvr_rword(obase - j, e - dc + j - 1)] = invalid;
+                }
+            }
+        }
+        if (active && compute && !(CVLR_SKIP & 5)) {
+            float *la = outl + (rowvox + (size_t)u) * D + e;
+            float *lb = la + D;
+            if (vec) {
+                if (aok) {
+                    reinterpret_cast<float4 *>(la)[0] = make_float4(ca[0], ca[1], ca[2], ca[3]);
+                    reinterpret_cast<float4 *>(la)[1] = make_float4(ca[4], ca[5], ca[6], ca[7]);
+                }
+                if (bok) {
+                    reinterpret_cast<float4 *>(lb)[0] = make_float4(cb[0], cb[1], cb[2], cb[3]);
+                    reinterpret_cast<float4 *>(lb)[1] = make_float4(cb[4], cb[5], cb[6], cb[7]);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    if (e + t < dc + nd) {
+                        if (aok) la[t] = ca[t];
+                        if (bok) lb[t] = cb[t];
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (k + 1 < nstrips) load_strip(q0 + CV_TX);
+        __syncthreads();
+        // [C] emit the completed R rows x' in [q0-dc-63, q0-dc] as full runs
+        if (!(CVLR_SKIP & 2) && lane < nd) {
+            for (int t = wave; t < CV_TX; t += CV_WAVES) {
+                const int xr = q0 - dc - (CV_TX - 1) + t;
+                if (xr >= 0 && xr < W) outr[(rowvox + xr) * D + dc + lane] = rring[cvr_rword(xr, lane)];
+            }
         }
     }
 }
@@ -572,22 +742,24 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
         dim3 grid(cdiv(W, CV_TX), H);
         if (layout == SDE_LAYOUT_DHW) {
             cv64_kernel<SDE_SIDE_LEFT, OUT_DHW><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid, out_left,
-                                                                       nullptr, nullptr, nullptr, nullptr);
+                                                                       nullptr, nullptr, nullptr);
         } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
-            // one pass: blocks past the row end (q < W + D - 1) only write R's invalid fill
-            const dim3 grid_lr(cdiv((int64_t)W + D - 1, CV_TX), H);
-            cv64_kernel<SDE_SIDE_LEFT, OUT_HWD_LR><<<grid_lr, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,
-                                                                              out_left, nullptr, nullptr, nullptr,
-                                                                              out_right);
+            // one row sweep per (row, 64-disparity chunk) writes both volumes
+            static const bool attr = [] {
+                return hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess;
+            }();
+            if (!attr) return SDE_ERR_LAUNCH;
+            const int nchunks = cdiv(D, CV_DC);
+            cvlr_row_kernel<<<dim3((unsigned)(nchunks * H)), 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
+                                                                         out_left, out_right);
         } else {
             if (sides & SDE_SIDE_LEFT)
                 cv64_kernel<SDE_SIDE_LEFT, OUT_HWD><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,
-                                                                           out_left, nullptr, nullptr, nullptr,
-                                                                           nullptr);
+                                                                           out_left, nullptr, nullptr, nullptr);
             if (sides & SDE_SIDE_RIGHT)
                 cv64_kernel<SDE_SIDE_RIGHT, OUT_HWD><<<grid, 256, 0, st>>>(fr, fl, H, W, 0, D, D, invalid,
-                                                                            out_right, nullptr, nullptr, nullptr,
-                                                                            nullptr);
+                                                                            out_right, nullptr, nullptr, nullptr);
         }
     } else {
         const int blocks = cdiv((int64_t)H * W, 256);
@@ -693,7 +865,7 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
     } else if (C == 64) {
         dim3 grid(cdiv(W, CV_TX), H);
         cv64_kernel<SDE_SIDE_LEFT, OUT_WTA><<<grid, 256, 0, st>>>(fl, fr, H, W, d0, d1, 0, -0.0f, nullptr,
-                                                                   min_cost, argmin, disp, nullptr);
+                                                                   min_cost, argmin, disp);
     } else {
         const int blocks = cdiv((int64_t)H * W, 256);
         cv_generic_kernel<OUT_WTA><<<blocks, 256, 0, st>>>(fl, fr, H, W, C, d0, d1, 0, SDE_SIDE_LEFT, -0.0f,

@@ -110,10 +110,14 @@ def test_disparity_shards_merge_bit_exact(gpu, oracle, nshards):
 def test_hwd_volumes_vs_oracle(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(11)
-    for (H, W, D) in [(3, 90, 64), (2, 70, 128), (2, 40, 100), (4, 300, 192), (2, 130, 200), (3, 64, 1)]:
+    for (H, W, D) in [(3, 90, 64), (2, 70, 128), (2, 40, 100), (4, 300, 192), (2, 130, 200), (3, 64, 1),
+                      (2, 1, 5), (2, 5, 64), (2, 128, 67), (1, 200, 130), (2, 63, 250), (1, 257, 190)]:
         fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
         fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
-        L, R = ops.cost_volume(dev(fl), dev(fr), D, layout="HWD", right=True, invalid=1.0)   # one pass, both
+        # one row sweep writes both; NaN-filled outputs catch any voxel it leaves unwritten
+        L = torch.full((H, W, D), float("nan"), device="cuda")
+        R = torch.full((H, W, D), float("nan"), device="cuda")
+        ops.cost_volume(dev(fl), dev(fr), D, layout="HWD", right=True, invalid=1.0, out_left=L, out_right=R)
         oL, oR = oracle.cost_volume_hwd(fl, fr, D, invalid=1.0)
         assert host(L).tobytes() == oL.tobytes()
         assert host(R).tobytes() == oR.tobytes()
