@@ -102,6 +102,16 @@ class Timer:
         self.pairs = []
 
 
+TOWER_ARITH = {
+    "fp32": "fp32 MFMA",
+    "bf16x6": "bf16x6: fp32 operands split exactly into 3 bf16 parts, 6 leading partial products on bf16 MFMA, "
+              "fp32 accumulation (fp32-level error)",
+    "f16x3": "f16x3: fp32 operands scaled by powers of two and split exactly into 2 fp16 parts, 3 leading partial "
+             "products on f16 MFMA, fp32 accumulation (~2^-22 per product; fp32-level error, checked vs the fp32 "
+             "MFMA tower in stages)",
+}
+
+
 def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: Timer):
     """One pass of the hot path, launched layer by layer so single kernels can be timed."""
     L = m.nlayers
@@ -110,13 +120,20 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     acts = [torch.empty((H + 2 * (L - 2), W + 2 * (L - 2), NF), dtype=torch.float32, device=m.device)
             for _ in range(2)]
 
+    # f16x3 bound words per image (what sde_tower_forward keeps in its workspace)
+    words = torch.zeros((2, L), dtype=torch.float32, device=m.device)
+
     def tower(i, timed):
         e_t = t_tower.start() if timed else None
         ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
-        # bf16x6: intermediate activations in the c-block-major layout, as sde_tower_forward runs them
-        cbl = m.tower_precision == "bf16x6"
+        # split arithmetics: intermediate activations in the c-block-major layout, as sde_tower_forward runs them
+        cbl = m.tower_precision in ("bf16x6", "f16x3")
+        wd = words[i]
+        if m.tower_precision == "f16x3":
+            wd.zero_()
+            ops.absmax(m.img_pad[i], wd[0:1])
         ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i], precision=m.tower_precision,
-                        out_cblock=cbl and L > 2)
+                        out_cblock=cbl and L > 2, in_absmax=wd[0:1], out_absmax=wd[1:2] if L > 2 else None)
         hin, win = H + 2 * L - 4, W + 2 * L - 4
         cur = 0
         for layer in range(3, L + 1):
@@ -128,7 +145,8 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
             e = t_conv.start() if (timed and layer == 3) else None
             ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision,
                             split=m.split[i] if (layer == L and m.split) else None,
-                            in_cblock=cbl, out_cblock=cbl and layer < L)
+                            in_cblock=cbl, out_cblock=cbl and layer < L, in_absmax=wd[layer - 2:layer - 1],
+                            out_absmax=wd[layer - 1:layer] if layer < L else None)
             if e is not None:
                 t_conv.stop(e)
             hin, win = hin - 2, win - 2
@@ -232,7 +250,7 @@ def main():
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--tower-precision", default="bf16x6", choices=["fp32", "bf16x6"])
+    ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
     args = ap.parse_args()
 
@@ -345,13 +363,15 @@ def main():
             stages["tower_ms_per_image"] = t_tower.mean_ms()
             stages["conv_layer3_ms"] = conv_ms
             stages["conv_fp32_equiv_TFLOPs"] = fl / (conv_ms * 1e-3) / 1e12
-            if m.tower_precision == "bf16x6":
-                # six bf16 partial products per fp32 product: the roof is the dense bf16 MFMA rate
-                ach = 6 * fl / (conv_ms * 1e-3) / 1e12
-                roof = {"kernel": "conv64_x6p_kernel<false,false,true,true> (tower layer 3, bf16x6)", "bound": "mfma",
+            if m.tower_precision in ("bf16x6", "f16x3"):
+                # 6 bf16 / 3 f16 partial products per fp32 product: the roof is the dense bf16/f16 MFMA rate
+                k, kt = (6, "bf16") if m.tower_precision == "bf16x6" else (3, "f16")
+                ach = k * fl / (conv_ms * 1e-3) / 1e12
+                roof = {"kernel": f"conv64_x6p_kernel<false,false,true,true,{str(kt == 'f16').lower()}> "
+                                  f"(tower layer 3, {m.tower_precision})", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,
                         "traffic": None,
-                        "per_launch": f"6 x {fl / 1e9:.2f} GFLOP bf16 (2*{hout}*{wout}*64*576 fp32-equivalent) "
+                        "per_launch": f"{k} x {fl / 1e9:.2f} GFLOP {kt} (2*{hout}*{wout}*64*576 fp32-equivalent) "
                                       f"over {conv_ms:.3f} ms"}
             else:
                 ach = fl / (conv_ms * 1e-3) / 1e12
@@ -359,13 +379,13 @@ def main():
                         "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
                         "traffic": None,
                         "per_launch": f"{fl / 1e9:.2f} GFLOP = 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
-            if m.tower_precision == "bf16x6":
+            if m.tower_precision != "fp32":
                 # the same features through the fp32-MFMA tower: max |difference| on this very image
                 ref = torch.empty_like(m.feat[0])
                 ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=ref, workspace=m.ws, precision="fp32")
                 ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=m.feat[0], workspace=m.ws,
-                                  precision="bf16x6")
-                stages["tower_bf16x6_vs_fp32_max_abs"] = float((ref - m.feat[0]).abs().max().item())
+                                  precision=m.tower_precision)
+                stages[f"tower_{m.tower_precision}_vs_fp32_max_abs"] = float((ref - m.feat[0]).abs().max().item())
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             kname = ("cv_wta_row_kernel + cv_wta_fixup_kernel (certified fused cost volume + WTA)"
@@ -396,9 +416,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_step, "ms_per_pair": ms_step / pairs_per_step * world
             if scaling == "weak" else ms_step,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
-            "tower_arith": ("bf16x6: fp32 operands split exactly into 3 bf16 parts, 6 leading partial products on "
-                            "bf16 MFMA, fp32 accumulation (fp32-level error)") if args.tower_precision == "bf16x6"
-                           else "fp32 MFMA",
+            "tower_arith": TOWER_ARITH[args.tower_precision],
             "data": "synthetic (seeded textured pair, band disparity field; synthetic He-normal tower weights)",
             "config": {"workload": args.workload, "H": H, "W": W, "D": D, "C": NF, "nlayers": NLAYERS,
                        "pipeline": what, "global_batch": pairs_per_step, "parallelism": par},

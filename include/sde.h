@@ -138,7 +138,12 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
 #define SDE_TOWER_FP32 0      /* v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation            */
 #define SDE_TOWER_BF16X6 1    /* fp32 operands split exactly into 3 bf16 parts, the 6 leading partial products
                                  on v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level error, 2.67x rate */
-/* sde_tower_layer only, with SDE_TOWER_BF16X6: intermediate activations in the c-block-major
+#define SDE_TOWER_F16X3 8     /* operands scaled by powers of two and split exactly into 2 fp16 parts, the 3
+                                 leading partial products on v_mfma_f32_32x32x16_f16, fp32 accumulation:
+                                 ~2^-22 relative per product (fp32-level), 5.3x the fp32 matrix rate.
+                                 The scalings need per-layer bound words: sde_tower_forward keeps them
+                                 in its workspace; single layers go through sde_tower_layer_scaled. */
+/* sde_tower_layer only, with SDE_TOWER_BF16X6 or SDE_TOWER_F16X3: intermediate activations in the c-block-major
  * layout [nf/16][h][w][16] that sde_tower_forward uses between layers (16-channel blocks
  * contiguous per pixel run).  IN: `in` of a layer >= 3; OUT: `out` of a layer < nlayers. */
 #define SDE_TOWER_IN_CBLOCK 2
@@ -178,6 +183,20 @@ int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, i
  */
 int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
                     float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm, void *stream);
+
+/*
+ * sde_tower_layer with the SDE_TOWER_F16X3 bound words (ignored by the other
+ * arithmetics): in_absmax -> device float, an upper bound of |input| (layer 2:
+ * of |image|; the kernel bounds conv1's output from it); out_absmax -> device
+ * float the launch atomically maxes its (non-negative) outputs into, zeroed by
+ * the caller (may be NULL for the last layer).
+ */
+int sde_tower_layer_scaled(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
+                           float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm,
+                           const float *in_absmax, float *out_absmax, void *stream);
+
+/* *absmax = max(*absmax, max |x[i]|) over n floats (float bits compared as integers; *absmax >= +0). */
+int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream);
 
 /*
  * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):

@@ -24,7 +24,7 @@ SDE_OK = 0
 SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
 SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
-SDE_TOWER_FP32, SDE_TOWER_BF16X6 = 0, 1
+SDE_TOWER_FP32, SDE_TOWER_BF16X6, SDE_TOWER_F16X3 = 0, 1, 8
 SDE_TOWER_IN_CBLOCK, SDE_TOWER_OUT_CBLOCK = 2, 4
 SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
 SDE_SGM_ACCUMULATE = 1
@@ -53,6 +53,9 @@ SIGNATURES = {
                                   c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sde_tower_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
+    "sde_tower_layer_scaled": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sde_absmax_f32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
                                   c_void_p]),

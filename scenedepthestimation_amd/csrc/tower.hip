@@ -21,6 +21,7 @@
 #include "sde_common.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 namespace sde {
@@ -36,8 +37,11 @@ constexpr int NF = 64;                   // feature maps (the reference's num_of
 constexpr int L1_FLOATS = NF + 9 * NF;           // bias + [tap][n]
 constexpr int LK_W = 9 * NF * NF;                // one [tap][n][c] plane, elements
 // layer k >= 2: bias f32 [64] | W f32 [tap][n][c] | bf16 parts (hi, mid, lo: W = hi+mid+lo) in A-fragment order
-// [mtile 2][cblock 4][tap 9][part 3][lane 64][8] for conv64_x6p_kernel
-constexpr int LK_FLOATS = NF + LK_W + 3 * LK_W / 2;
+// [mtile 2][cblock 4][tap 9][part 3][lane 64][8] for conv64_x6p_kernel | fp16 parts of W * 2^tau (hi, lo)
+// [mtile 2][cblock 4][tap 9][part 2][lane 64][8] for the F16 variant | F16 header {2^-tau, conv1 L1 bound,
+// max |b1|, 0} (the conv1 terms are used by layer 2, which computes conv1)
+constexpr int LK_F16 = NF + LK_W + 3 * LK_W / 2;   // float offset of the fp16 parts
+constexpr int LK_FLOATS = LK_F16 + LK_W + 4;
 
 // float2 slot of channel pair `pair` (0..31) of pixel/row `p` in a swizzled 64-float row
 __device__ __forceinline__ int pslot(int p, int pair) { return p * 32 + (pair ^ (p & 31)); }
@@ -259,9 +263,29 @@ __global__ __launch_bounds__(512) void conv64_mfma_kernel(const float *__restric
 // Inter-layer activations use a c-block-major layout [4][h][w][16] (IN_CB /
 // OUT_CB) so a stage reads contiguous 64-B pixel runs; the last layer writes the
 // reference's [h][w][64].
+//
+// F16 (SDE_TOWER_F16X3): the same kernel with every operand split into TWO fp16
+// parts after a power-of-two scaling, x*2^s = h + l (h = fp16(x*2^s), l =
+// fp16(x*2^s - h), the residual exact in f32), and the three partial products
+// h*h' + h*l' + l*h' on v_mfma_f32_32x32x16_f16.  fp16's 11-bit significand
+// makes two parts carry 22 bits: the dropped l*l' term is < 2^-22 |ab| and each
+// part's rounding 2^-23 relative -- the error of a few fp32 roundings per
+// product, at half the MFMAs of bf16x6.  The scalings keep the parts in fp16's
+// normal range without any chance of overflow:
+// * weights: 2^tau per layer from the host (max |w| * 2^tau in [2^14, 2^15));
+// * activations: 2^sigma per launch from a device word holding an upper bound
+//   of |input| (the previous layer's epilogue atomically maxes its ReLU outputs
+//   into it; for layer 2 the word holds max |image| and the kernel bounds conv1's
+//   output by max|image| * max_n sum_t |w1[t][n]| + max |b1|), so that
+//   bound * 2^sigma lies in [2^14, 2^15) < 65504.  Values far below the bound
+//   lose relative precision only as fp16 subnormals do: absolute error
+//   <= 2^-25 * 2^-sigma, i.e. <= 2^-40 of the layer's largest input.
+// The epilogue multiplies the accumulators by 2^-(tau+sigma) (exact).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
 {
@@ -271,6 +295,18 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
     const float r2 = r1 - (float)m;
     l = (__bf16)r2;
 }
+
+// Profiling builds only (tools/tower_variants.sh): TOWER_DIAG bits switch parts of the
+// persistent kernel off -- 1 stager HBM loads, 2 all stager work, 4 the MFMAs, 8 the MFMA
+// waves' LDS fragment reads, 16 the middle layers' output stores, 32 the per-c-block barriers, 64 the A-fragment reloads
+// (timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
+// out[2 * blockIdx.x + {0, 1}] (clock check).  0 in the library.
+#ifndef XP_RING_F16
+#define XP_RING_F16 3
+#endif
+#ifndef TOWER_DIAG
+#define TOWER_DIAG 0
+#endif
 
 constexpr int XP_TY = 16, XP_TX = 32;             // output tile
 constexpr int XP_IY = XP_TY + 2, XP_IX = XP_TX + 2;
@@ -301,6 +337,30 @@ __device__ __forceinline__ void xp_put(char *sb, int u, float4 v)
     *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
     *reinterpret_cast<uint2 *>(dst + 2 * XP_PLANE) = __builtin_bit_cast(uint2, p1);
     *reinterpret_cast<uint2 *>(dst + 4 * XP_PLANE) = __builtin_bit_cast(uint2, p2);
+}
+
+// F16: scale by 2^sigma (s), split into two fp16 parts, store planes (part, channel half).
+__device__ __forceinline__ void xp_put16(char *sb, int u, float4 v, float s)
+{
+    const int px = u >> 2, chunk = u & 3;
+    f16x4 p0, p1;
+    const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const _Float16 h = (_Float16)xs[e];
+        p0[e] = h;
+        p1[e] = (_Float16)(xs[e] - (float)h);
+    }
+    char *dst = sb + (chunk >> 1) * XP_PLANE + px * 16 + (chunk & 1) * 8;
+    *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
+    *reinterpret_cast<uint2 *>(dst + 2 * XP_PLANE) = __builtin_bit_cast(uint2, p1);
+}
+
+template <bool F16>
+__device__ __forceinline__ void xp_store(char *sb, int u, float4 v, float s)
+{
+    if (F16) xp_put16(sb, u, v, s);
+    else xp_put(sb, u, v);
 }
 
 // One stage unit of activations (zero outside the input).
@@ -344,14 +404,15 @@ __device__ __forceinline__ float4 xp_conv1(const float *__restrict__ img, int Hi
 }
 
 // Stager waves: fill one stage with c-block cb of tile t.
-template <bool FIRST, bool IN_CB>
+template <bool FIRST, bool IN_CB, bool F16>
 __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, int Hin, int Win,
-                                        const float *__restrict__ w1blob, int t, int tiles_x, int cb, int st)
+                                        const float *__restrict__ w1blob, int t, int tiles_x, int cb, int st, float s)
 {
     // opaque to the optimiser: stops loop-invariant code motion from hoisting the per-unit
     // address arithmetic of all units out of the tile loop (it would pin ~40 VGPRs that the
     // MFMA waves' accumulators need)
     asm volatile("" : "+v"(st));
+    if (TOWER_DIAG & 2) return;
     const int ty0 = (t / tiles_x) * XP_TY, tx0 = (t % tiles_x) * XP_TX;
     if (FIRST) {
         // the thread's chunk is st & 3 for every unit (XP_STAGERS is a multiple of 4)
@@ -363,7 +424,7 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
 #pragma unroll 2
         for (int i = 0; i < XP_UPT; i++) {
             const int u = st + i * XP_STAGERS;
-            if (u < XP_UNITS) xp_put(sb, u, xp_conv1(in, Hin, Win, w, b, ty0, tx0, u));
+            if (u < XP_UNITS) xp_store<F16>(sb, u, xp_conv1(in, Hin, Win, w, b, ty0, tx0, u), s);
         }
     } else {
         // two batches of 5 loads in flight (the stagers have time; registers are shared
@@ -375,14 +436,66 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
 #pragma unroll
             for (int i = 0; i < HB; i++) {
                 const int u = st + (b0 + i) * XP_STAGERS;
-                v[i] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (TOWER_DIAG & 1) v[i] = make_float4(u * 1e-3f, 0.5f, 0.25f, (float)cb);
+                else v[i] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int i = 0; i < HB; i++) {
                 const int u = st + (b0 + i) * XP_STAGERS;
-                if (u < XP_UNITS) xp_put(sb, u, v[i]);
+                if (u < XP_UNITS) xp_store<F16>(sb, u, v[i], s);
             }
         }
+    }
+}
+
+// Stager waves' own loop (non-FIRST layers): the pipeline of (tile, c-block) steps the MFMA
+// waves consume, one stage ahead, with the HBM loads of step i+2 issued before step i+1's
+// units are split and stored -- every load has a whole c-block period to land.  Runs the
+// same barriers as the MFMA waves: one per c-block, plus LAST's two per tile.
+template <bool IN_CB, bool LAST, bool F16>
+__device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restrict__ in, int Hin, int Win, int tiles_x,
+                                               int ntiles, int st, float s)
+{
+    const int tile0 = blockIdx.x, gstride = gridDim.x;
+    const int nsteps = ((ntiles - 1 - tile0) / gstride + 1) * XP_NCB;
+    auto load = [&](float4 (&v)[XP_UPT], int i) {
+        const int t = tile0 + (i / XP_NCB) * gstride, cb = i % XP_NCB;
+        const int ty0 = (t / tiles_x) * XP_TY, tx0 = (t % tiles_x) * XP_TX;
+#pragma unroll
+        for (int k = 0; k < XP_UPT; k++) {
+            const int u = st + k * XP_STAGERS;
+            if (TOWER_DIAG & 1) v[k] = make_float4(u * 1e-3f, 0.5f, 0.25f, (float)cb);
+            else v[k] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](const float4 (&v)[XP_UPT], int i) {
+        if (TOWER_DIAG & 2) return;
+        char *sb = xsm + (i & 1) * XP_STAGE;
+#pragma unroll
+        for (int k = 0; k < XP_UPT; k++) {
+            const int u = st + k * XP_STAGERS;
+            if (u < XP_UNITS) xp_store<F16>(sb, u, v[k], s);
+        }
+    };
+    auto sync_step = [&](int i) {
+        if (LAST && i % XP_NCB == XP_NCB - 1) { __syncthreads(); __syncthreads(); }
+        if (!(TOWER_DIAG & 32)) __syncthreads();
+    };
+    float4 ra[XP_UPT], rb[XP_UPT];
+    load(ra, 0);
+    store(ra, 0);
+    if (nsteps > 1) load(ra, 1);
+    __syncthreads();
+    // step i: the MFMA waves consume stage i & 1; here step i+1 is stored and step i+2 loaded
+#pragma unroll 1
+    for (int i = 0; i < nsteps; i += 2) {
+        if (i + 2 < nsteps) load(rb, i + 2);
+        if (i + 1 < nsteps) store(ra, i + 1);
+        sync_step(i);
+        if (i + 1 >= nsteps) break;
+        if (i + 3 < nsteps) load(ra, i + 3);
+        if (i + 2 < nsteps) store(rb, i + 2);
+        sync_step(i + 1);
     }
 }
 
@@ -390,26 +503,37 @@ struct XpFrag {
     bf16x8 p[3];
 };
 
+// A fragments of one (c-block, tap): NP = 3 bf16 parts, or 2 fp16 parts (F16; the blob holds
+// [mtile][cblock][tap][part NP][lane][8] for each arithmetic).  Unused parts stay untouched.
+template <int NP>
 __device__ __forceinline__ XpFrag xp_afrag(const uint4 *__restrict__ wf, int mt, int cb, int tap, int lane)
 {
-    const uint4 *src = wf + ((size_t)((mt * XP_NCB + cb) * 9 + tap) * 3) * 64 + lane;
+    const uint4 *src = wf + ((size_t)((mt * XP_NCB + cb) * 9 + tap) * NP) * 64 + lane;
     XpFrag f;
 #pragma unroll
-    for (int q = 0; q < 3; q++) f.p[q] = __builtin_bit_cast(bf16x8, src[q * 64]);
+    for (int q = 0; q < NP; q++) f.p[q] = __builtin_bit_cast(bf16x8, src[q * 64]);
     return f;
 }
 
-// B fragments (three parts) of one row-step.
+// B fragments (three parts; two for F16) of one row-step.
 struct XpB {
     bf16x8 p[3];
 };
 
+template <int NP>
 __device__ __forceinline__ XpB xp_bfrag(const char *b)
 {
     XpB f;
 #pragma unroll
-    for (int q = 0; q < 3; q++) f.p[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(b + 2 * q * XP_PLANE));
+    for (int q = 0; q < NP; q++)
+        f.p[q] = (TOWER_DIAG & 8) ? __builtin_bit_cast(bf16x8, make_uint4((uint32_t)(uintptr_t)b, q, 1u, 2u))
+                                  : __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(b + 2 * q * XP_PLANE));
     return f;
+}
+
+__device__ __forceinline__ floatx16 mfma_h(bf16x8 a, bf16x8 b, floatx16 c)
+{
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
 // One c-block for one MFMA wave: 9 taps x 8 rows = 72 row-steps of 6 MFMAs (small terms
@@ -418,14 +542,17 @@ __device__ __forceinline__ XpB xp_bfrag(const char *b)
 // bounds the live registers (8 accumulators = 128 of the 256 a wave may hold at 2 waves
 // per SIMD).  A fragments for tap t+1 are requested when tap t starts.  Rows past the
 // output edge run on zero-filled input and are discarded by the epilogue.
+template <bool F16>
 __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ROWS], XpFrag (&an)[2], const uint4 *__restrict__ wf,
                                           int mt, int cb, int ncb, int lane, const char *sb)
 {
     constexpr int NS = 9 * XP_ROWS;
-    XpB ring[3];
+    constexpr int NP = F16 ? 2 : 3;
+    constexpr int RD = F16 ? XP_RING_F16 : 3;   // ring depth: fragments read RD-1 row-steps ahead
+    XpB ring[RD];
     auto boff = [&](int s) { return ((s / XP_ROWS / 3 + s % XP_ROWS) * XP_IX + (s / XP_ROWS) % 3) * 16; };
-    ring[0] = xp_bfrag(sb + boff(0));
-    ring[1] = xp_bfrag(sb + boff(1));
+#pragma unroll
+    for (int k = 0; k < RD - 1; k++) ring[k] = xp_bfrag<NP>(sb + boff(k));
     XpFrag a = an[0];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -434,27 +561,52 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ROWS], XpFrag (&an)
             // A fragments two taps ahead: an[0] = A(tap + 1), an[1] = A(tap + 2)
             if (tap > 0) a = an[0];
             an[0] = an[1];
-            an[1] = tap < 7 ? xp_afrag(wf, mt, cb, tap + 2, lane) : xp_afrag(wf, mt, ncb, tap - 7, lane);
+            if (TOWER_DIAG & 64) an[1] = an[0];
+            else an[1] = tap < 7 ? xp_afrag<NP>(wf, mt, cb, tap + 2, lane) : xp_afrag<NP>(wf, mt, ncb, tap - 7, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
-        const XpB &b = ring[s % 3];
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc[r], 0, 0, 0);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc[r], 0, 0, 0);
-        if (s + 2 < NS) ring[(s + 2) % 3] = xp_bfrag(sb + boff(s + 2));
+        const XpB &b = ring[s % RD];
+        if (TOWER_DIAG & 4) {
+#pragma unroll
+            for (int q = 0; q < NP; q++) asm volatile("" ::"v"(b.p[q]), "v"(a.p[q]));   // keep the fragments live
+        } else if (F16) {
+            acc[r] = mfma_h(a.p[1], b.p[0], acc[r]);
+            acc[r] = mfma_h(a.p[0], b.p[1], acc[r]);
+            acc[r] = mfma_h(a.p[0], b.p[0], acc[r]);
+        } else {
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc[r], 0, 0, 0);
+        }
+        if (s + RD - 1 < NS) ring[(s + RD - 1) % RD] = xp_bfrag<NP>(sb + boff(s + RD - 1));
     }
 }
 
-template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB>
+// F16 scalings of one launch (see above): s = 2^sigma for the stagers, unscale = 2^-(tau+sigma).
+// hdr: the layer blob's F16 header {2^-tau, max_n sum_t |w1[t][n]|, max |b1|, 0}.
+__device__ __forceinline__ void xp_scales(bool first, const float *__restrict__ in_amax, const float *__restrict__ hdr,
+                                          float &s, float &unscale)
+{
+    const float m = *in_amax;
+    const float bound = first ? fmaf(m, hdr[1], hdr[2]) : m;
+    int e = 0;   // bound in [2^e, 2^(e+1)); a zero, subnormal or non-finite bound leaves sigma = 14
+    if (bound >= 1.17549435e-38f && bound <= 3.40282347e38f) e = (int)((__float_as_uint(bound) >> 23) & 255u) - 127;
+    const int sigma = min(max(14 - e, -100), 100);
+    s = ldexpf(1.0f, sigma);
+    unscale = ldexpf(hdr[0], -sigma);
+}
+
+template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB, bool F16>
 __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ w1blob,
                                                          const float *__restrict__ wkblob,
                                                          float *__restrict__ out, int Hout, int Wout,
                                                          uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
-                                                         float *__restrict__ onrm, int tiles_x, int ntiles)
+                                                         float *__restrict__ onrm, int tiles_x, int ntiles,
+                                                         const float *__restrict__ in_amax, float *__restrict__ out_amax)
 {
     extern __shared__ __attribute__((aligned(16))) char xsm[];
     float *red0 = reinterpret_cast<float *>(xsm + 2 * XP_STAGE);   // [2 mt][16 rows][32 px]
@@ -466,19 +618,29 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     const bool mfma_wave = wave < 4;            // waves 4..7 stage the input
     const int mt = wave & 1, g = (wave >> 1) & 1;
     const int st = tid - XP_STAGERS;            // stager thread index (valid when !mfma_wave)
+    constexpr int NP = F16 ? 2 : 3;
     const float *bias = wkblob;
-    const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + NF + LK_W);
+    const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + (F16 ? LK_F16 : NF + LK_W));
     // B fragment: plane (part, h), input row 8g + r + ky, pixel j + kx
     const int bbase = (lane >> 5) * XP_PLANE + ((XP_ROWS * g) * XP_IX + (lane & 31)) * 16;
 
     int tile = blockIdx.x;
     if (tile >= ntiles) return;
+    const uint64_t t_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t r_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
+    float s = 1.0f, unscale = 1.0f;
+    if (F16) xp_scales(FIRST, in_amax, wkblob + LK_F16 + LK_W, s, unscale);
+    float amax = 0.0f;   // F16, !LAST: running max of this wave's stored outputs
+    if (!FIRST && !LAST && !mfma_wave) {
+        xp_stager_loop<IN_CB, LAST, F16>(xsm, in, Hin, Win, tiles_x, ntiles, st, s);
+        return;
+    }
     XpFrag an[2];
     if (mfma_wave) {
-        an[0] = xp_afrag(wf, mt, 0, 0, lane);
-        an[1] = xp_afrag(wf, mt, 0, 1, lane);
+        an[0] = xp_afrag<NP>(wf, mt, 0, 0, lane);
+        an[1] = xp_afrag<NP>(wf, mt, 0, 1, lane);
     }
-    else xp_fill<FIRST, IN_CB>(xsm, in, Hin, Win, w1blob, tile, tiles_x, 0, st);
+    else xp_fill<FIRST, IN_CB, F16>(xsm, in, Hin, Win, w1blob, tile, tiles_x, 0, st, s);
     __syncthreads();
 
     int cur = 0;
@@ -493,9 +655,9 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
             const int ntile = cb + 1 < XP_NCB ? tile : tile + (int)gridDim.x;
             const int ncb = (cb + 1) & (XP_NCB - 1);
             if (mfma_wave) {
-                xp_cblock(acc, an, wf, mt, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
+                xp_cblock<F16>(acc, an, wf, mt, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
             } else if (ntile < ntiles) {
-                xp_fill<FIRST, IN_CB>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, tiles_x, ncb, st);
+                xp_fill<FIRST, IN_CB, F16>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, tiles_x, ncb, st, s);
             }
             if (cb == XP_NCB - 1) {
                 // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
@@ -507,6 +669,13 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                 float bv[16];
 #pragma unroll
                 for (int i = 0; i < 16; i++) bv[i] = bias[mt * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+                if (F16 && mfma_wave) {
+                    // undo the power-of-two scalings (exact)
+#pragma unroll
+                    for (int r = 0; r < XP_ROWS; r++)
+#pragma unroll
+                        for (int i = 0; i < 16; i++) acc[r][i] *= unscale;
+                }
                 if (!LAST) {
                     if (mfma_wave) {
 #pragma unroll
@@ -519,10 +688,11 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                                                                  fmaxf(acc[r][4 * q + 1] + bv[4 * q + 1], 0.f),
                                                                  fmaxf(acc[r][4 * q + 2] + bv[4 * q + 2], 0.f),
                                                                  fmaxf(acc[r][4 * q + 3] + bv[4 * q + 3], 0.f));
+                                    if (F16) amax = fmaxf(amax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
                                     const int c = mt * 32 + 8 * q + 4 * h;
                                     float *dst = OUT_CB ? out + (((size_t)(c >> 4) * Hout + y) * Wout + x) * 16 + (c & 15)
                                                         : out + ((size_t)y * Wout + x) * NF + c;
-                                    *reinterpret_cast<float4 *>(dst) = o;
+                                    if (!(TOWER_DIAG & 16) || o.x == -1.0f) *reinterpret_cast<float4 *>(dst) = o;
                                 }
                             }
                         }
@@ -592,10 +762,46 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                     }
                 }
             }
-            __syncthreads();
+            if (!(TOWER_DIAG & 32)) __syncthreads();
             cur ^= 1;
         }
     }
+    if ((TOWER_DIAG & 128) && tid == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        out[2 * blockIdx.x] = (float)(t1 - t_start);
+        out[2 * blockIdx.x + 1] = (float)(r1 - r_start);
+    }
+    if (F16 && !LAST && mfma_wave) {
+        // outputs are >= +0 (ReLU): their float bits order like their values
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax), __float_as_uint(amax));
+    }
+}
+
+// max |x| over n floats, atomically maxed (as float bits) into *amax (F16 tower scaling):
+// float4 grid-stride loads, one atomic per workgroup.
+__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ x, int64_t n, float *__restrict__ amax)
+{
+    float m = 0.0f;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+    const int64_t head = std::min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(x) & 15)) / 4 & 3);
+    if (tid < head) m = fabsf(x[tid]);
+    const float4 *x4 = reinterpret_cast<const float4 *>(x + head);
+    const int64_t n4 = (n - head) / 4;
+    for (int64_t i = tid; i < n4; i += nt) {
+        const float4 v = x4[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int64_t i = head + 4 * n4 + tid; i < n; i += nt) m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        atomicMax(reinterpret_cast<unsigned int *>(amax),
+                  __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // nlayers == 1: conv1 + L2 normalisation only (no ReLU on the last layer).
@@ -701,6 +907,7 @@ static float bf2f(uint16_t h)
     return f;
 }
 
+static constexpr int64_t TOWER_AMAX_BYTES = 256;   // 64 bound words (nlayers <= 64)
 static constexpr size_t TW_SMEM = (size_t)(TW_NPIX * 32 + 2 * NF * 32) * sizeof(float2);
 
 SDE_EXPORT int64_t sde_tower_packed_floats(int nlayers, int nf)
@@ -718,10 +925,38 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
     for (int n = 0; n < NF; n++) o[n] = biases[0][n];
     for (int i = 0; i < 9 * NF; i++) o[NF + i] = hwio[0][i];
     o += L1_FLOATS;
+    // conv1 output bound terms for the F16 scaling (layer 2 computes conv1)
+    float l1 = 0.0f, bmax = 0.0f;
+    for (int n = 0; n < NF; n++) {
+        double s = 0.0;
+        for (int t = 0; t < 9; t++) s += std::fabs((double)hwio[0][t * NF + n]);
+        l1 = std::max(l1, (float)(s * (1.0 + 1e-6)));   // rounded up: a bound of the f32 conv1
+        bmax = std::max(bmax, std::fabs(biases[0][n]));
+    }
     for (int l = 1; l < nlayers; l++) {
         for (int n = 0; n < NF; n++) o[n] = biases[l][n];
         float *w = o + NF;
         uint16_t *pl = reinterpret_cast<uint16_t *>(w + LK_W);
+        // F16 parts of W * 2^tau, max |W| * 2^tau in [2^14, 2^15)
+        float wmax = 0.0f;
+        for (size_t i = 0; i < (size_t)LK_W; i++) wmax = std::max(wmax, std::fabs(hwio[l][i]));
+        const int tau = (wmax > 0.0f && std::isfinite(wmax)) ? std::min(std::max(14 - std::ilogb(wmax), -100), 100) : 0;
+        _Float16 *ph = reinterpret_cast<_Float16 *>(o + LK_F16);
+        float *hdr = o + LK_F16 + LK_W;
+        hdr[0] = std::ldexp(1.0f, -tau);
+        hdr[1] = l1;
+        hdr[2] = bmax;
+        hdr[3] = 0.0f;
+        for (int tap = 0; tap < 9; tap++)
+            for (int c = 0; c < NF; c++)
+                for (int n = 0; n < NF; n++) {
+                    const float x = std::ldexp(hwio[l][((size_t)tap * NF + c) * NF + n], tau);
+                    const _Float16 h0 = (_Float16)x;
+                    const _Float16 parts[2] = {h0, (_Float16)(x - (float)h0)};
+                    const int mt = n >> 5, cb = c >> 4, ln = ((c >> 3) & 1) * 32 + (n & 31);
+                    for (int q = 0; q < 2; q++)
+                        ph[((((size_t)(mt * XP_NCB + cb) * 9 + tap) * 2 + q) * 64 + ln) * 8 + (c & 7)] = parts[q];
+                }
         for (int tap = 0; tap < 9; tap++)
             for (int c = 0; c < NF; c++)
                 for (int n = 0; n < NF; n++) {
@@ -747,10 +982,10 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
 SDE_EXPORT int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf)
 {
     if (H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return -1;
-    if (nlayers <= 2) return 0;
-    // two ping-pong activation buffers sized for layer 2's output
+    if (nlayers == 1) return 0;
+    // two ping-pong activation buffers sized for layer 2's output, then the F16X3 bound words
     const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
-    return 2 * h2 * w2 * NF * (int64_t)sizeof(float);
+    return (nlayers > 2 ? 2 * h2 * w2 * NF * (int64_t)sizeof(float) : 0) + TOWER_AMAX_BYTES;
 }
 
 static void set_tower_attrs()
@@ -761,8 +996,9 @@ static void set_tower_attrs()
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
-#define SDE_X6P_ATTR(F, L, I, O) (void)hipFuncSetAttribute((const void *)conv64_x6p_kernel<F, L, I, O>, \
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, XP_SMEM)
+#define SDE_X6P_ATTR1(F, L, I, O, H) (void)hipFuncSetAttribute((const void *)conv64_x6p_kernel<F, L, I, O, H>, \
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize, XP_SMEM)
+#define SDE_X6P_ATTR(F, L, I, O) SDE_X6P_ATTR1(F, L, I, O, false); SDE_X6P_ATTR1(F, L, I, O, true)
     SDE_X6P_ATTR(true, false, false, true);
     SDE_X6P_ATTR(true, false, false, false);
     SDE_X6P_ATTR(true, true, false, false);
@@ -772,6 +1008,7 @@ static void set_tower_attrs()
     SDE_X6P_ATTR(false, false, false, true);
     SDE_X6P_ATTR(false, true, true, false);
     SDE_X6P_ATTR(false, true, false, false);
+#undef SDE_X6P_ATTR1
 #undef SDE_X6P_ATTR
     done = true;
 }
@@ -791,36 +1028,42 @@ static int cu_count()
 
 // One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
 // layer > 2 -> one 64->64 conv on Hin x Win x 64 activations.  Output (Hin-4|Hin-2) x ... x 64.
-// in_cb / out_cb: activations in the c-block-major layout [4][h][w][16] (bf16x6 path only).
+// in_cb / out_cb: activations in the c-block-major layout [4][h][w][16] (bf16x6 / f16x3 paths).
+// F16X3: in_amax = bound of |input| (|image| for layer 2), out_amax = max of the ReLU outputs
+// (zeroed by the caller; unused by the last layer).
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
                          int flags, uint16_t *ohi, uint16_t *olo, float *onrm, bool in_cb, bool out_cb,
-                         hipStream_t st)
+                         const float *in_amax, float *out_amax, hipStream_t st)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
-    const bool x6 = (flags & SDE_TOWER_BF16X6) != 0;
+    const bool f16 = (flags & SDE_TOWER_F16X3) != 0;
+    const bool x6 = f16 || (flags & SDE_TOWER_BF16X6) != 0;
     const float *w1 = packed;
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
     if (x6) {
         const int tiles_x = cdiv(wout, XP_TX), ntiles = tiles_x * cdiv(hout, XP_TY);
         const int grid = std::min(ntiles, cu_count());
-#define SDE_X6P(F, L, I, O) conv64_x6p_kernel<F, L, I, O><<<grid, 512, XP_SMEM, st>>>( \
+#define SDE_X6P(F, L, I, O, H) conv64_x6p_kernel<F, L, I, O, H><<<grid, 512, XP_SMEM, st>>>( \
         in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
-        (L) ? onrm : nullptr, tiles_x, ntiles)
-        if (layer == 2) {
-            if (last) SDE_X6P(true, true, false, false);
-            else if (out_cb) SDE_X6P(true, false, false, true);
-            else SDE_X6P(true, false, false, false);
-        } else if (last) {
-            if (in_cb) SDE_X6P(false, true, true, false);
-            else SDE_X6P(false, true, false, false);
-        } else {
-            if (in_cb && out_cb) SDE_X6P(false, false, true, true);
-            else if (in_cb) SDE_X6P(false, false, true, false);
-            else if (out_cb) SDE_X6P(false, false, false, true);
-            else SDE_X6P(false, false, false, false);
+        (L) ? onrm : nullptr, tiles_x, ntiles, in_amax, out_amax)
+#define SDE_X6P_ALL(H)                                                      \
+        if (layer == 2) {                                                   \
+            if (last) SDE_X6P(true, true, false, false, H);                 \
+            else if (out_cb) SDE_X6P(true, false, false, true, H);          \
+            else SDE_X6P(true, false, false, false, H);                     \
+        } else if (last) {                                                  \
+            if (in_cb) SDE_X6P(false, true, true, false, H);                \
+            else SDE_X6P(false, true, false, false, H);                     \
+        } else {                                                            \
+            if (in_cb && out_cb) SDE_X6P(false, false, true, true, H);      \
+            else if (in_cb) SDE_X6P(false, false, true, false, H);          \
+            else if (out_cb) SDE_X6P(false, false, false, true, H);         \
+            else SDE_X6P(false, false, false, false, H);                    \
         }
+        if (f16) { SDE_X6P_ALL(true) } else { SDE_X6P_ALL(false) }
+#undef SDE_X6P_ALL
 #undef SDE_X6P
         return;
     }
@@ -832,19 +1075,48 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 #undef SDE_CONV
 }
 
+static bool tower_flags_ok(int flags, bool layer_api)
+{
+    const int prec = flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3);
+    if (prec == (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) return false;
+    const int layout = SDE_TOWER_IN_CBLOCK | SDE_TOWER_OUT_CBLOCK;
+    if (!layer_api) return (flags & ~(SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) == 0;
+    if (flags & ~(SDE_TOWER_BF16X6 | SDE_TOWER_F16X3 | layout)) return false;
+    return !((flags & layout) && prec == 0);
+}
+
+SDE_EXPORT int sde_tower_layer_scaled(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf,
+                                      int layer, float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo,
+                                      float *feat_norm, const float *in_absmax, float *out_absmax, void *stream)
+{
+    if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
+    if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
+    if (!tower_flags_ok(flags, true)) return SDE_ERR_ARG;
+    const bool in_cb = (flags & SDE_TOWER_IN_CBLOCK) != 0, out_cb = (flags & SDE_TOWER_OUT_CBLOCK) != 0;
+    if ((in_cb && layer == 2) || (out_cb && layer == nlayers)) return SDE_ERR_ARG;
+    if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
+    if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax))) return SDE_ERR_ARG;
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, in_cb, out_cb,
+                 in_absmax, out_absmax, as_stream(stream));
+    return launch_status();
+}
+
 SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
                                float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm,
                                void *stream)
 {
-    if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers) return SDE_ERR_ARG;
-    if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
-    if (flags & ~(SDE_TOWER_BF16X6 | SDE_TOWER_IN_CBLOCK | SDE_TOWER_OUT_CBLOCK)) return SDE_ERR_ARG;
-    const bool in_cb = (flags & SDE_TOWER_IN_CBLOCK) != 0, out_cb = (flags & SDE_TOWER_OUT_CBLOCK) != 0;
-    if ((in_cb || out_cb) && !(flags & SDE_TOWER_BF16X6)) return SDE_ERR_ARG;
-    if ((in_cb && layer == 2) || (out_cb && layer == nlayers)) return SDE_ERR_ARG;
-    if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
-    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, in_cb, out_cb,
-                 as_stream(stream));
+    if (flags & SDE_TOWER_F16X3) return SDE_ERR_ARG;   // needs the bound words: sde_tower_layer_scaled
+    return sde_tower_layer_scaled(in, Hin, Win, packed, nlayers, nf, layer, out, flags, feat_hi, feat_lo, feat_norm,
+                                  nullptr, nullptr, stream);
+}
+
+SDE_EXPORT int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream)
+{
+    if (!absmax || n < 0) return SDE_ERR_ARG;
+    if (n == 0) return SDE_OK;
+    if (!x) return SDE_ERR_ARG;
+    const int blocks = (int)std::min<int64_t>(256, cdiv(n, 256 * 16));
+    absmax_kernel<<<blocks, 256, 0, as_stream(stream)>>>(x, n, absmax);
     return launch_status();
 }
 
@@ -855,7 +1127,7 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
     if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
     if (nlayers == 1 && (feat_hi || feat_norm)) return SDE_ERR_ARG;
     if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
-    if (flags & ~SDE_TOWER_BF16X6) return SDE_ERR_ARG;
+    if (!tower_flags_ok(flags, false)) return SDE_ERR_ARG;
     const int64_t need = sde_tower_workspace_bytes(H, W, nlayers, nf);
     if (need > 0 && (!workspace || workspace_bytes < need)) return SDE_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
@@ -865,22 +1137,31 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
         return launch_status();
     }
     float *buf[2] = {nullptr, nullptr};
+    const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
     if (nlayers > 2) {
-        const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
         buf[0] = reinterpret_cast<float *>(workspace);
         buf[1] = buf[0] + h2 * w2 * NF;
     }
+    // F16X3 bound words: amax[l - 2] bounds |input of layer l|
+    float *amax = reinterpret_cast<float *>(static_cast<char *>(workspace) + (nlayers > 2 ? 2 * h2 * w2 * NF * 4 : 0));
+    const bool f16 = (flags & SDE_TOWER_F16X3) != 0;
+    if (f16) {
+        if (nlayers > (int)(TOWER_AMAX_BYTES / 4)) return SDE_ERR_ARG;
+        if (hipMemsetAsync(amax, 0, TOWER_AMAX_BYTES, st) != hipSuccess) return SDE_ERR_LAUNCH;
+        const int rc = sde_absmax_f32(img_pad, (int64_t)Hp * Wp, amax, stream);
+        if (rc != SDE_OK) return rc;
+    }
     int hin = Hp, win = Wp;
-    // intermediate activations in the c-block-major layout on the bf16x6 path
-    const bool cbl = (flags & SDE_TOWER_BF16X6) != 0;
+    // intermediate activations in the c-block-major layout on the split paths
+    const bool cbl = (flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) != 0;
     launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, feat_hi, feat_lo, feat_norm,
-                 false, cbl && nlayers > 2, st);
+                 false, cbl && nlayers > 2, amax, amax + 1, st);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
         launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, cbl,
-                     cbl && l < nlayers, st);
+                     cbl && l < nlayers, amax + (l - 2), amax + (l - 1), st);
         hin -= 2; win -= 2;
         cur ^= 1;
     }

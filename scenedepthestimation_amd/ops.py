@@ -215,7 +215,7 @@ def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
     return int(lib.sde_tower_workspace_bytes(H, W, nlayers, nf))
 
 
-TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6}
+TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6, "f16x3": _lib.SDE_TOWER_F16X3}
 
 
 def _split_ptrs(split, shape):
@@ -248,7 +248,8 @@ def feature_split(feat, split=None):
 def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None, precision: str = "fp32",
                   split=None):
     """img_pad: f32 [H+2L, W+2L] -> L2-normalised features f32 [H, W, nf].
-    precision: 'fp32' (fp32 MFMA) or 'bf16x6' (exact 3-way bf16 split, 6 partial products, fp32 accumulate).
+    precision: 'fp32' (fp32 MFMA), 'bf16x6' (exact 3-way bf16 split, 6 partial products, fp32 accumulate) or
+    'f16x3' (power-of-two scaled exact 2-way fp16 split, 3 partial products, fp32 accumulate).
     split: optional (hi, lo, norm) buffers the last layer's epilogue fills (certified cost volume input)."""
     Hp, Wp = img_pad.shape
     H, W = Hp - 2 * nlayers, Wp - 2 * nlayers
@@ -270,12 +271,21 @@ def tower_forward(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspa
     return out
 
 
+def absmax(x, out):
+    """out (f32 [1] device) = max(out, max |x|) (sde_absmax_f32)."""
+    check(lib.sde_absmax_f32(_need(x, "absmax input"), x.numel(), _need(out, "absmax word", shape=(1,)), _stream()),
+          "sde_absmax_f32")
+    return out
+
+
 def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
-                in_cblock: bool = False, out_cblock: bool = False):
+                in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
     """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
-    in_cblock / out_cblock (bf16x6): intermediate activations in the c-block-major layout
+    in_cblock / out_cblock (bf16x6, f16x3): intermediate activations in the c-block-major layout
     [nf/16][h][w][16] that tower_forward uses between layers (tensors keep their [h, w, nf]
-    shape; only the element order differs)."""
+    shape; only the element order differs).
+    in_absmax / out_absmax (f16x3): f32 [1] device words -- a bound of |input| (|image| for layer
+    2) and the word this layer maxes its outputs into (zeroed by the caller)."""
     flags = TOWER_PRECISIONS[precision]
     if in_cblock:
         flags |= _lib.SDE_TOWER_IN_CBLOCK
@@ -287,11 +297,13 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precis
     else:
         Hin, Win, _ = inp.shape
         oshape = (Hin - 2, Win - 2, nf)
-    check(lib.sde_tower_layer(_need(inp, "layer input"), Hin, Win,
-                              _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
-                              nlayers, nf, layer, _need(out, "layer output", shape=oshape),
-                              flags, *_split_ptrs(split, oshape[:2]), _stream()),
-          "sde_tower_layer")
+    pin = _need(in_absmax, "in_absmax", shape=(1,)) if in_absmax is not None else None
+    pout = _need(out_absmax, "out_absmax", shape=(1,)) if out_absmax is not None else None
+    check(lib.sde_tower_layer_scaled(_need(inp, "layer input"), Hin, Win,
+                                     _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
+                                     nlayers, nf, layer, _need(out, "layer output", shape=oshape),
+                                     flags, *_split_ptrs(split, oshape[:2]), pin, pout, _stream()),
+          "sde_tower_layer_scaled")
     return out
 
 

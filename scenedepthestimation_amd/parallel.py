@@ -83,7 +83,7 @@ def gather_row_bands(band: torch.Tensor, full: torch.Tensor, world: int, group=N
 class DisparityShardedMatcher:
     """Config 5: features from row bands + all-gather, disparity-sharded fused CV/WTA + all-gather merge."""
 
-    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="bf16x6"):
+    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="f16x3"):
         from .pipeline import StereoMatcher
         self.H, self.W, self.D = H, W, D
         self.rank, self.world, self.group = rank, world, group

@@ -24,7 +24,7 @@ from . import mc_cnn, ops
 
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
-                 nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "bf16x6",
+                 nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "f16x3",
                  cv_mode: str = "certified", cbca_iters: int = 0, cbca_L1: int = 14, cbca_tau: float = 0.02,
                  emit_split: bool = False):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)

@@ -40,7 +40,8 @@ def test_tower_packing_matches_layout():
     hw, hb = mc_cnn.layer_lists(w, L)
     packed = ops.pack_tower_weights(hw, hb)
     LW = 9 * 64 * 64
-    LK = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 parts
+    LF = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 parts
+    LK = LF + LW + 4                              # | 2 fp16 parts of W * 2^tau | F16 header
     assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * LK
     assert np.array_equal(packed[:64], hb[0])
     assert np.array_equal(packed[64:640], hw[0].reshape(-1))
@@ -52,7 +53,7 @@ def test_tower_packing_matches_layout():
         assert np.array_equal(blob, ref)
         # bf16 parts in A-fragment order [mtile 2][cblock 4][tap 9][part 3][lane 64][8]:
         # lane = ((c % 16) >= 8) * 32 + n % 32, element c % 8 (conv64_x6p_kernel)
-        frag = packed[base + 64 + LW:base + LK].view(np.uint16).reshape(2, 4, 9, 3, 2, 32, 8)
+        frag = packed[base + 64 + LW:base + LF].view(np.uint16).reshape(2, 4, 9, 3, 2, 32, 8)
         # -> [part][tap][n = mt*32 + lane%32][c = cb*16 + half*8 + e]
         planes = frag.transpose(3, 2, 0, 5, 1, 4, 6).reshape(3, 9, 64, 64)
         as_f32 = (planes.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
@@ -60,8 +61,20 @@ def test_tower_packing_matches_layout():
         assert np.array_equal(as_f32.sum(0), ref.astype(np.float64))
         hi = as_f32[0]
         assert np.all(np.abs(ref - hi) <= np.abs(ref) * 2.0 ** -8)
-    assert ops.tower_workspace_bytes(100, 80, 5) == 2 * 106 * 86 * 64 * 4
-    assert ops.tower_workspace_bytes(100, 80, 2) == 0
+        # F16X3: header {2^-tau, conv1 L1 bound, max |b1|, 0}; two fp16 parts of W * 2^tau in the
+        # same fragment order with 2 parts, max |W| * 2^tau in [2^14, 2^15)
+        hdr = packed[base + LF + LW:base + LK]
+        tau = -int(np.log2(hdr[0]))
+        assert hdr[0] == 2.0 ** -tau and 2.0 ** 14 <= np.abs(ref).max() * 2.0 ** tau < 2.0 ** 15
+        l1 = np.abs(hw[0].reshape(9, 64).astype(np.float64)).sum(0).max()
+        assert l1 <= hdr[1] <= l1 * (1 + 4e-6) and hdr[2] == np.abs(hb[0]).max() and hdr[3] == 0
+        f16 = packed[base + LF:base + LF + LW].view(np.float16).reshape(2, 4, 9, 2, 2, 32, 8)
+        hparts = f16.transpose(3, 2, 0, 5, 1, 4, 6).reshape(2, 9, 64, 64).astype(np.float64)
+        scaled = ref.astype(np.float64) * 2.0 ** tau
+        assert np.array_equal(hparts[0], scaled.astype(np.float16).astype(np.float64))   # RNE hi part
+        assert np.all(np.abs(hparts.sum(0) - scaled) <= np.abs(scaled) * 2.0 ** -22 + 2.0 ** -25)
+    assert ops.tower_workspace_bytes(100, 80, 5) == 2 * 106 * 86 * 64 * 4 + 256
+    assert ops.tower_workspace_bytes(100, 80, 2) == 256
 
 
 def test_argument_validation_without_gpu():
@@ -82,6 +95,12 @@ def test_argument_validation_without_gpu():
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 4, N, N, N, N) == ERR           # bad flags
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 0, 1, N, N, N) == ERR           # hi without lo
     assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, 0, N, N, N, N) == ERR                      # layer 1
+    assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 3, 1, 8, N, N, N, N) == ERR                      # f16x3: bounds
+    assert lib.sde_tower_layer_scaled(1, 8, 8, 1, 5, 64, 3, 1, 8, N, N, N, N, 1, N) == ERR         # no out bound
+    assert lib.sde_tower_layer_scaled(1, 8, 8, 1, 5, 64, 3, 1, 9, N, N, N, 1, 1, N) == ERR         # two precisions
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 9, N, N, N, N) == ERR           # two precisions
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 8 | 2, N, N, N, N) == ERR       # layout flag
+    assert lib.sde_absmax_f32(N, 4, 1, N) == ERR
     assert lib.sde_feature_split(1, 10, 32, 1, 1, 1, N) == ERR                                     # C != 64
     assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace
     assert lib.sde_cv_wta_split(1, 1, N, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 1 << 20, N) == ERR

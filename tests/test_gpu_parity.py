@@ -139,7 +139,7 @@ def test_generic_channel_counts(gpu, golden, golden_cases):
 # ----------------------------------------------------------------------------
 # tower
 # ----------------------------------------------------------------------------
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 20, 37), (5, 41, 70), (3, 17, 33), (2, 9, 40), (1, 6, 7)])
 def test_tower_vs_oracle(gpu, oracle, nlayers, H, W, precision):
     from scenedepthestimation_amd import mc_cnn, ops
@@ -167,15 +167,39 @@ def test_tower_precision_report(gpu, oracle):
     ref = oracle.tower_forward(img, hw, hb)
     packed = dev(ops.pack_tower_weights(hw, hb))
     errs = {}
-    for prec in ("fp32", "bf16x6"):
+    for prec in ("fp32", "bf16x6", "f16x3"):
         out = host(ops.tower_forward(dev(img), packed, L, precision=prec))
         errs[prec] = float(np.abs(out - ref).max())
     print("tower max abs err vs fp64:", errs)
-    assert errs["fp32"] < 1e-5 and errs["bf16x6"] < 1e-5
+    assert errs["fp32"] < 1e-5 and errs["bf16x6"] < 1e-5 and errs["f16x3"] < 1e-5
 
 
+@pytest.mark.parametrize("scale", [1e-6, 1e-3, 1e3, 1e12])
+def test_tower_f16x3_dynamic_range(gpu, oracle, scale):
+    """f16x3 scales operands by powers of two from device bound words: an image and weights far
+    outside fp16's range (tiny or huge) keep fp32-level accuracy (relative to the fp64 tower) and
+    never overflow.  The last layer L2-normalises, so the features are scale-free."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    rng = np.random.default_rng(5)
+    H, W, L = 24, 70, 5
+    w = mc_cnn.synthetic_weights(L, seed=9)
+    hw, hb = mc_cnn.layer_lists(w, L)
+    hw = [x * np.float32(scale ** (1 / L)) for x in hw]
+    hb = [x * np.float32(scale ** ((k + 1) / L)) for k, x in enumerate(hb)]
+    img = np.zeros((H + 2 * L, W + 2 * L), np.float32)
+    img[L:-L, L:-L] = rng.standard_normal((H, W)).astype(np.float32)
+    ref = oracle.tower_forward(img, hw, hb)
+    packed = dev(ops.pack_tower_weights(hw, hb))
+    out = host(ops.tower_forward(dev(img), packed, L, precision="f16x3"))
+    assert np.isfinite(out).all()
+    err = float(np.abs(out - ref).max())
+    print("f16x3 scale", scale, err)
+    assert err < 1e-5
+
+
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 700, 530), (3, 300, 1100), (2, 530, 517)])
-def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W):
+def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W, precision):
     """Sizes with more output tiles than CUs (the persistent bf16x6 kernel's tile loop, partial
     edge tiles, the c-block-major intermediate layout): bf16x6 vs the fp32-MFMA kernel, both
     fp32-level accurate, agree to ~1e-6."""
@@ -186,11 +210,11 @@ def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W):
     img = torch.zeros((H + 2 * nlayers, W + 2 * nlayers), device="cuda")
     img[nlayers:-nlayers, nlayers:-nlayers] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
     a = ops.tower_forward(img, packed, nlayers, precision="fp32")
-    b = ops.tower_forward(img, packed, nlayers, precision="bf16x6")
+    b = ops.tower_forward(img, packed, nlayers, precision=precision)
     torch.cuda.synchronize()
     assert torch.isfinite(b).all()
     err = float((a - b).abs().max())
-    print("bf16x6 vs fp32 tower", (nlayers, H, W), err)
+    print(precision, "vs fp32 tower", (nlayers, H, W), err)
     assert err < 1e-5
 
 
@@ -202,14 +226,17 @@ def test_tower_layer_api_matches_forward(gpu):
     packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=9), L)))
     img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
     img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
-    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True)):
+    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True), ("f16x3", False), ("f16x3", True)):
         full = ops.tower_forward(img, packed, L, precision=prec)
         x = img
+        words = torch.zeros(L, device="cuda")          # f16x3 bound words, as tower_forward keeps them
+        ops.absmax(img, words[0:1])
         for layer in range(2, L + 1):
             shrink = 4 if layer == 2 else 2
             y = torch.empty((x.shape[0] - shrink, x.shape[1] - shrink, 64), device="cuda")
             ops.tower_layer(x, packed, L, layer, y, precision=prec, in_cblock=cbl and layer > 2,
-                            out_cblock=cbl and layer < L)
+                            out_cblock=cbl and layer < L, in_absmax=words[layer - 2:layer - 1],
+                            out_absmax=words[layer - 1:layer] if layer < L else None)
             x = y
         torch.cuda.synchronize()
         # same arithmetic in the same order whatever the activation layout: bit-identical
@@ -596,3 +623,18 @@ def test_cv_wta_split_matches_exact(gpu, oracle):
         assert host(mn).tobytes() == host(em).tobytes()
         fl, fr = host(m.feat[0]), host(m.feat[1])
         assert np.array_equal(host(disp), oracle.WTA1(oracle.compute_cost_volume(fl, fr, D)))
+
+
+@pytest.mark.parametrize("off,n", [(0, 0), (0, 1), (1, 3), (3, 1000), (2, 4097), (0, 1 << 20)])
+def test_absmax(gpu, off, n):
+    """sde_absmax_f32 (the f16x3 tower's image bound): unaligned heads and ragged tails."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(n + off)
+    x = rng.standard_normal(off + n).astype(np.float32) * 3
+    if n:
+        x[off + rng.integers(n)] = -50.0
+    xd = dev(x)[off:]
+    word = torch.full((1,), 1.5, device="cuda")
+    ops.absmax(xd, word)
+    want = max(1.5, float(np.abs(x[off:]).max())) if n else 1.5
+    assert float(word.cpu()[0]) == want
