@@ -116,44 +116,53 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     """One pass of the hot path, launched layer by layer so single kernels can be timed."""
     L = m.nlayers
     H, W = m.H, m.W
-    # activation ping-pong buffers for layers 3..L (layer 2 output is (H+2(L-2)) x ...)
-    acts = [torch.empty((H + 2 * (L - 2), W + 2 * (L - 2), NF), dtype=torch.float32, device=m.device)
+    # activation ping-pong buffers for layers 3..L, both images (layer 2 output is (H+2(L-2)) x ...)
+    acts = [torch.empty((2 * (H + 2 * (L - 2)) * (W + 2 * (L - 2)) * NF,), dtype=torch.float32, device=m.device)
             for _ in range(2)]
-
-    # f16x3 bound words per image (what sde_tower_forward keeps in its workspace)
+    # f16x3 bound words per image (what sde_tower_forward_batch keeps in its workspace)
     words = torch.zeros((2, L), dtype=torch.float32, device=m.device)
+    batched = m.split is None
 
-    def tower(i, timed):
+    def tower_pair(timed):
+        """Preprocess both images, then the tower layer by layer with both images per launch
+        (sde_tower_layer_batch = what sde_tower_forward_batch launches), layer 3 timed."""
         e_t = t_tower.start() if timed else None
-        ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
+        for i in range(2):
+            ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
+        if not batched:   # split planes requested: per-image launches
+            m.features_from_padded()
+            if e_t is not None:
+                t_tower.stop(e_t)
+            return
         # split arithmetics: intermediate activations in the c-block-major layout, as sde_tower_forward runs them
         cbl = m.tower_precision in ("bf16x6", "f16x3")
-        wd = words[i]
         if m.tower_precision == "f16x3":
-            wd.zero_()
-            ops.absmax(m.img_pad[i], wd[0:1])
-        ops.tower_layer(m.img_pad[i], m.packed, L, 2, acts[0] if L > 2 else m.feat[i], precision=m.tower_precision,
-                        out_cblock=cbl and L > 2, in_absmax=wd[0:1], out_absmax=wd[1:2] if L > 2 else None)
+            words.zero_()
+            for i in range(2):
+                ops.absmax(m.img_pad[i], words[i, 0:1])
         hin, win = H + 2 * L - 4, W + 2 * L - 4
+        first_out = acts[0][: 2 * hin * win * NF].view(2, hin, win, NF) if L > 2 else m.feat2
+        ops.tower_layer_batch(m.img_pad2, m.packed, L, 2, first_out, precision=m.tower_precision,
+                              out_cblock=cbl and L > 2, in_absmax=words[:, 0:1],
+                              out_absmax=words[:, 1:2] if L > 2 else None)
         cur = 0
         for layer in range(3, L + 1):
             if layer == L:
-                o = m.feat[i]
+                o = m.feat2
             else:   # a contiguous prefix of the ping-pong buffer, viewed at this layer's size
-                o = acts[cur ^ 1].view(-1)[: (hin - 2) * (win - 2) * NF].view(hin - 2, win - 2, NF)
-            src = acts[cur].view(-1)[: hin * win * NF].view(hin, win, NF)
+                o = acts[cur ^ 1][: 2 * (hin - 2) * (win - 2) * NF].view(2, hin - 2, win - 2, NF)
+            src = acts[cur][: 2 * hin * win * NF].view(2, hin, win, NF)
             e = t_conv.start() if (timed and layer == 3) else None
-            ops.tower_layer(src, m.packed, L, layer, o, precision=m.tower_precision,
-                            split=m.split[i] if (layer == L and m.split) else None,
-                            in_cblock=cbl, out_cblock=cbl and layer < L, in_absmax=wd[layer - 2:layer - 1],
-                            out_absmax=wd[layer - 1:layer] if layer < L else None)
+            ops.tower_layer_batch(src, m.packed, L, layer, o, precision=m.tower_precision,
+                                  in_cblock=cbl, out_cblock=cbl and layer < L, in_absmax=words[:, layer - 2:layer - 1],
+                                  out_absmax=words[:, layer - 1:layer] if layer < L else None)
             if e is not None:
                 t_conv.stop(e)
             hin, win = hin - 2, win - 2
             cur ^= 1
         if e_t is not None:
             t_tower.stop(e_t)
-        m.split_valid = m.split is not None
+        m.split_valid = False
 
     if what == "tower+cbca+sgm":
         def step_sgm(timed=False):
@@ -170,8 +179,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
 
     def step(timed=False):
         if what == "tower+cv_wta":
-            tower(0, timed)
-            tower(1, timed)
+            tower_pair(timed)
         e = t_cv.start() if timed else None
         m.cost_wta()
         if e is not None:
@@ -359,8 +367,8 @@ def main():
             conv_ms = t_conv.mean_ms()
             hout = H + 2 * (NLAYERS - 3)
             wout = W + 2 * (NLAYERS - 3)
-            fl = conv_flops(hout, wout)
-            stages["tower_ms_per_image"] = t_tower.mean_ms()
+            fl = 2 * conv_flops(hout, wout)   # one launch = both images of the pair
+            stages["tower_ms_pair"] = t_tower.mean_ms()
             stages["conv_layer3_ms"] = conv_ms
             stages["conv_fp32_equiv_TFLOPs"] = fl / (conv_ms * 1e-3) / 1e12
             if m.tower_precision in ("bf16x6", "f16x3"):
@@ -371,14 +379,14 @@ def main():
                                   f"(tower layer 3, {m.tower_precision})", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,
                         "traffic": None,
-                        "per_launch": f"{k} x {fl / 1e9:.2f} GFLOP {kt} (2*{hout}*{wout}*64*576 fp32-equivalent) "
+                        "per_launch": f"{k} x {fl / 1e9:.2f} GFLOP {kt} (2 images x 2*{hout}*{wout}*64*576 fp32-equivalent) "
                                       f"over {conv_ms:.3f} ms"}
             else:
                 ach = fl / (conv_ms * 1e-3) / 1e12
                 roof = {"kernel": "conv64_mfma_kernel<false,false> (tower layer 3, fp32)", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
                         "traffic": None,
-                        "per_launch": f"{fl / 1e9:.2f} GFLOP = 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
+                        "per_launch": f"{fl / 1e9:.2f} GFLOP = 2 images x 2*{hout}*{wout}*64*576 over {conv_ms:.3f} ms"}
             if m.tower_precision != "fp32":
                 # the same features through the fp32-MFMA tower: max |difference| on this very image
                 ref = torch.empty_like(m.feat[0])

@@ -176,6 +176,18 @@ int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, i
                       uint16_t *feat_lo, float *feat_norm, void *stream);
 
 /*
+ * sde_tower_forward over nimg images of one size in one set of launches (the
+ * split arithmetics tile the whole batch in one persistent grid: fewer launches,
+ * less tail imbalance).  img_pad: [nimg][H+2*nlayers][W+2*nlayers]; feat:
+ * [nimg][H][W][nf]; feat_hi / feat_lo: [nimg][H][W][nf]; feat_norm: [nimg][H][W].
+ * Each image gets the same result as sde_tower_forward on it alone.
+ */
+int64_t sde_tower_batch_workspace_bytes(int H, int W, int nimg, int nlayers, int nf);
+int sde_tower_forward_batch(const float *img_pad, int nimg, int H, int W, const float *packed, int nlayers, int nf,
+                            float *feat, void *workspace, int64_t workspace_bytes, int flags, uint16_t *feat_hi,
+                            uint16_t *feat_lo, float *feat_norm, void *stream);
+
+/*
  * One layer of the tower as a single kernel launch (for per-layer timing and
  * pipelining): layer == 2 -> conv1+conv2 fused, `in` = padded image Hin x Win
  * floats, out (Hin-4) x (Win-4) x nf; layer in 3..nlayers -> `in` = Hin x Win x
@@ -194,6 +206,16 @@ int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int 
 int sde_tower_layer_scaled(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
                            float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm,
                            const float *in_absmax, float *out_absmax, void *stream);
+
+/*
+ * sde_tower_layer_scaled over nimg images per launch (no split outputs): image i
+ * reads in + i * in_stride, writes out + i * out_stride (floats; the last layer's
+ * out_stride must be (Hin-2)*(Win-2)*nf) and uses bound words in_absmax /
+ * out_absmax + i * amax_stride.
+ */
+int sde_tower_layer_batch(const float *in, int nimg, int64_t in_stride, int Hin, int Win, const float *packed,
+                          int nlayers, int nf, int layer, float *out, int64_t out_stride, int flags,
+                          const float *in_absmax, float *out_absmax, int amax_stride, void *stream);
 
 /* *absmax = max(*absmax, max |x[i]|) over n floats (float bits compared as integers; *absmax >= +0). */
 int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream);

@@ -318,7 +318,9 @@ constexpr int XP_STAGERS = 256;                   // threads of the stager waves
 constexpr int XP_UPT = (XP_UNITS + XP_STAGERS - 1) / XP_STAGERS;   // units per stager thread (10)
 constexpr int XP_ROWS = 8;                        // output rows per MFMA wave
 constexpr int XP_RED = 2 * 2 * XP_TY * XP_TX * 4; // LAST: two per-M-tile partial-sum exchanges
-constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + XP_RED;
+constexpr int XP_WX = XP_IX + 2, XP_WIN = (XP_IY + 2) * XP_WX;   // FIRST: image window of a tile (20 x 36)
+// two stages | LAST's partial-sum exchanges | FIRST: one image window per stager wave
+constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + XP_RED + 4 * XP_WIN * sizeof(float);
 constexpr int XP_NCB = NF / 16;                   // c-blocks per pixel
 
 // Split 4 channels and store them into the stage's six planes.
@@ -337,6 +339,23 @@ __device__ __forceinline__ void xp_put(char *sb, int u, float4 v)
     *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
     *reinterpret_cast<uint2 *>(dst + 2 * XP_PLANE) = __builtin_bit_cast(uint2, p1);
     *reinterpret_cast<uint2 *>(dst + 4 * XP_PLANE) = __builtin_bit_cast(uint2, p2);
+}
+
+// Tiles of a launch over a batch of images of one size: tile t -> image t / tiles_img, then
+// row-major 16 x 32 output tiles.  Strides are per image (floats; pixels for the split outputs;
+// floats between the images' F16 bound-word arrays).
+struct XpBatch {
+    int tiles_x, tiles_img, ntiles;
+    int64_t in_stride, out_stride, pix_stride;
+    int amax_stride;
+};
+
+__device__ __forceinline__ void xp_tile(const XpBatch &bt, int t, int &img, int &ty0, int &tx0)
+{
+    img = t / bt.tiles_img;
+    const int tl = t - img * bt.tiles_img;
+    ty0 = (tl / bt.tiles_x) * XP_TY;
+    tx0 = (tl % bt.tiles_x) * XP_TX;
 }
 
 // F16: scale by 2^sigma (s), split into two fp16 parts, store planes (part, channel half).
@@ -381,7 +400,8 @@ __device__ __forceinline__ float4 xp_load(const float *__restrict__ in, int Hin,
 
 // conv1 (Cin = 1, 3x3, bias, ReLU) of the padded image for one stage unit; w = the 9 taps x
 // 4 channels of the unit's chunk, b = their biases (a stager thread's chunk is fixed).
-__device__ __forceinline__ float4 xp_conv1(const float *__restrict__ img, int Hin, int Win, const float4 (&w)[9],
+// The image values come from the stager wave's LDS window of the tile (win[iy][ix], 20 x 36).
+__device__ __forceinline__ float4 xp_conv1(const float *win, int Hin, int Win, const float4 (&w)[9],
                                            float4 b, int ty0, int tx0, int u)
 {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -390,9 +410,10 @@ __device__ __forceinline__ float4 xp_conv1(const float *__restrict__ img, int Hi
     const int y = ty0 + iy, x = tx0 + ix;
     if (y < Hin - 2 && x < Win - 2) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        const float *wp = win + iy * XP_WX + ix;
 #pragma unroll
         for (int t = 0; t < 9; t++) {
-            const float im = img[(size_t)(y + t / 3) * Win + x + t % 3];
+            const float im = wp[(t / 3) * XP_WX + t % 3];
             s0 = fmaf(im, w[t].x, s0);
             s1 = fmaf(im, w[t].y, s1);
             s2 = fmaf(im, w[t].z, s2);
@@ -406,15 +427,34 @@ __device__ __forceinline__ float4 xp_conv1(const float *__restrict__ img, int Hi
 // Stager waves: fill one stage with c-block cb of tile t.
 template <bool FIRST, bool IN_CB, bool F16>
 __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, int Hin, int Win,
-                                        const float *__restrict__ w1blob, int t, int tiles_x, int cb, int st, float s)
+                                        const float *__restrict__ w1blob, int t, const XpBatch &bt, int cb, int st,
+                                        float s, float *win)
 {
     // opaque to the optimiser: stops loop-invariant code motion from hoisting the per-unit
     // address arithmetic of all units out of the tile loop (it would pin ~40 VGPRs that the
     // MFMA waves' accumulators need)
     asm volatile("" : "+v"(st));
     if (TOWER_DIAG & 2) return;
-    const int ty0 = (t / tiles_x) * XP_TY, tx0 = (t % tiles_x) * XP_TX;
+    int img, ty0, tx0;
+    xp_tile(bt, t, img, ty0, tx0);
+    in += img * bt.in_stride;
     if (FIRST) {
+        if (cb == 0) {
+            // a new tile: this wave's copy of the tile's image window (wave-private: no barrier;
+            // a wave's LDS accesses complete in order)
+            const int lane = st & 63;
+#pragma unroll
+            for (int k = 0; k < (XP_WIN + 63) / 64; k++) {
+                const int idx = lane + 64 * k;
+                if (idx < XP_WIN) {
+                    const int iy = idx / XP_WX, ix = idx - iy * XP_WX;
+                    const int y = ty0 + iy, x = tx0 + ix;
+                    win[idx] = (y < Hin && x < Win) ? in[(size_t)y * Win + x] : 0.0f;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the window's LDS writes have landed
+            __builtin_amdgcn_wave_barrier();
+        }
         // the thread's chunk is st & 3 for every unit (XP_STAGERS is a multiple of 4)
         const int n0 = cb * 16 + (st & 3) * 4;
         const float4 b = *reinterpret_cast<const float4 *>(w1blob + n0);
@@ -424,7 +464,7 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
 #pragma unroll 2
         for (int i = 0; i < XP_UPT; i++) {
             const int u = st + i * XP_STAGERS;
-            if (u < XP_UNITS) xp_store<F16>(sb, u, xp_conv1(in, Hin, Win, w, b, ty0, tx0, u), s);
+            if (u < XP_UNITS) xp_store<F16>(sb, u, xp_conv1(win, Hin, Win, w, b, ty0, tx0, u), s);
         }
     } else {
         // two batches of 5 loads in flight (the stagers have time; registers are shared
@@ -448,28 +488,52 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
     }
 }
 
+// F16 scalings of one tile (see above): s = 2^sigma for the stagers, unscale = 2^-(tau+sigma).
+// hdr: the layer blob's F16 header {2^-tau, max_n sum_t |w1[t][n]|, max |b1|, 0}.
+__device__ __forceinline__ void xp_scales(bool first, const float *__restrict__ in_amax, const float *__restrict__ hdr,
+                                          float &s, float &unscale)
+{
+    const float m = *in_amax;
+    const float bound = first ? fmaf(m, hdr[1], hdr[2]) : m;
+    int e = 0;   // bound in [2^e, 2^(e+1)); a zero, subnormal or non-finite bound leaves sigma = 14
+    if (bound >= 1.17549435e-38f && bound <= 3.40282347e38f) e = (int)((__float_as_uint(bound) >> 23) & 255u) - 127;
+    const int sigma = min(max(14 - e, -100), 100);
+    s = ldexpf(1.0f, sigma);
+    unscale = ldexpf(hdr[0], -sigma);
+}
+
 // Stager waves' own loop (non-FIRST layers): the pipeline of (tile, c-block) steps the MFMA
 // waves consume, one stage ahead, with the HBM loads of step i+2 issued before step i+1's
 // units are split and stored -- every load has a whole c-block period to land.  Runs the
 // same barriers as the MFMA waves: one per c-block, plus LAST's two per tile.
 template <bool IN_CB, bool LAST, bool F16>
-__device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restrict__ in, int Hin, int Win, int tiles_x,
-                                               int ntiles, int st, float s)
+__device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restrict__ in, int Hin, int Win,
+                                               const XpBatch &bt, int st, const float *__restrict__ in_amax,
+                                               const float *__restrict__ hdr)
 {
     const int tile0 = blockIdx.x, gstride = gridDim.x;
-    const int nsteps = ((ntiles - 1 - tile0) / gstride + 1) * XP_NCB;
+    const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * XP_NCB;
     auto load = [&](float4 (&v)[XP_UPT], int i) {
         const int t = tile0 + (i / XP_NCB) * gstride, cb = i % XP_NCB;
-        const int ty0 = (t / tiles_x) * XP_TY, tx0 = (t % tiles_x) * XP_TX;
+        int img, ty0, tx0;
+        xp_tile(bt, t, img, ty0, tx0);
+        const float *src = in + img * bt.in_stride;
 #pragma unroll
         for (int k = 0; k < XP_UPT; k++) {
             const int u = st + k * XP_STAGERS;
             if (TOWER_DIAG & 1) v[k] = make_float4(u * 1e-3f, 0.5f, 0.25f, (float)cb);
-            else v[k] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            else v[k] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
+    int sc_img = -1;
+    float s = 1.0f, unscale = 1.0f;
     auto store = [&](const float4 (&v)[XP_UPT], int i) {
         if (TOWER_DIAG & 2) return;
+        const int im = (tile0 + (i / XP_NCB) * gstride) / bt.tiles_img;
+        if (F16 && im != sc_img) {   // the tile's image changed: its bound word (tiles run image-major)
+            xp_scales(false, in_amax + im * bt.amax_stride, hdr, s, unscale);
+            sc_img = im;
+        }
         char *sb = xsm + (i & 1) * XP_STAGE;
 #pragma unroll
         for (int k = 0; k < XP_UPT; k++) {
@@ -585,32 +649,20 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ROWS], XpFrag (&an)
     }
 }
 
-// F16 scalings of one launch (see above): s = 2^sigma for the stagers, unscale = 2^-(tau+sigma).
-// hdr: the layer blob's F16 header {2^-tau, max_n sum_t |w1[t][n]|, max |b1|, 0}.
-__device__ __forceinline__ void xp_scales(bool first, const float *__restrict__ in_amax, const float *__restrict__ hdr,
-                                          float &s, float &unscale)
-{
-    const float m = *in_amax;
-    const float bound = first ? fmaf(m, hdr[1], hdr[2]) : m;
-    int e = 0;   // bound in [2^e, 2^(e+1)); a zero, subnormal or non-finite bound leaves sigma = 14
-    if (bound >= 1.17549435e-38f && bound <= 3.40282347e38f) e = (int)((__float_as_uint(bound) >> 23) & 255u) - 127;
-    const int sigma = min(max(14 - e, -100), 100);
-    s = ldexpf(1.0f, sigma);
-    unscale = ldexpf(hdr[0], -sigma);
-}
-
 template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB, bool F16>
 __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ w1blob,
                                                          const float *__restrict__ wkblob,
                                                          float *__restrict__ out, int Hout, int Wout,
                                                          uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
-                                                         float *__restrict__ onrm, int tiles_x, int ntiles,
+                                                         float *__restrict__ onrm, XpBatch bt,
                                                          const float *__restrict__ in_amax, float *__restrict__ out_amax)
 {
     extern __shared__ __attribute__((aligned(16))) char xsm[];
     float *red0 = reinterpret_cast<float *>(xsm + 2 * XP_STAGE);   // [2 mt][16 rows][32 px]
     float *red1 = red0 + 2 * XP_TY * XP_TX;
+    // FIRST: the stager wave's image window
+    float *win = reinterpret_cast<float *>(xsm + 2 * XP_STAGE + XP_RED) + ((threadIdx.x >> 6) & 3) * XP_WIN;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -625,14 +677,27 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     const int bbase = (lane >> 5) * XP_PLANE + ((XP_ROWS * g) * XP_IX + (lane & 31)) * 16;
 
     int tile = blockIdx.x;
-    if (tile >= ntiles) return;
+    if (tile >= bt.ntiles) return;
     const uint64_t t_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t r_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
-    float s = 1.0f, unscale = 1.0f;
-    if (F16) xp_scales(FIRST, in_amax, wkblob + LK_F16 + LK_W, s, unscale);
-    float amax = 0.0f;   // F16, !LAST: running max of this wave's stored outputs
+    const float *hdr = wkblob + LK_F16 + LK_W;
+    // F16 scalings of a tile (per image: each image has its own bound words; re-read only when
+    // the tile's image changes -- tiles run image-major)
+    int sc_img = -1;
+    float sc_s = 1.0f, sc_u = 1.0f;
+    auto scales = [&](int t, float &sc, float &usc) {
+        if (F16) {
+            const int im = t / bt.tiles_img;
+            if (im != sc_img) {
+                xp_scales(FIRST, in_amax + im * bt.amax_stride, hdr, sc_s, sc_u);
+                sc_img = im;
+            }
+        }
+        sc = sc_s;
+        usc = sc_u;
+    };
     if (!FIRST && !LAST && !mfma_wave) {
-        xp_stager_loop<IN_CB, LAST, F16>(xsm, in, Hin, Win, tiles_x, ntiles, st, s);
+        xp_stager_loop<IN_CB, LAST, F16>(xsm, in, Hin, Win, bt, st, in_amax, hdr);
         return;
     }
     XpFrag an[2];
@@ -640,12 +705,18 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         an[0] = xp_afrag<NP>(wf, mt, 0, 0, lane);
         an[1] = xp_afrag<NP>(wf, mt, 0, 1, lane);
     }
-    else xp_fill<FIRST, IN_CB, F16>(xsm, in, Hin, Win, w1blob, tile, tiles_x, 0, st, s);
+    else {
+        float s0, u0;
+        scales(tile, s0, u0);
+        xp_fill<FIRST, IN_CB, F16>(xsm, in, Hin, Win, w1blob, tile, bt, 0, st, s0, win);
+    }
     __syncthreads();
 
     int cur = 0;
-    for (; tile < ntiles; tile += gridDim.x) {
-        const int ty0 = (tile / tiles_x) * XP_TY, tx0 = (tile % tiles_x) * XP_TX;
+    for (; tile < bt.ntiles; tile += gridDim.x) {
+        int img, ty0, tx0;
+        xp_tile(bt, tile, img, ty0, tx0);
+        float *const outi = out + img * bt.out_stride;
         floatx16 acc[XP_ROWS];
 #pragma unroll
         for (int r = 0; r < XP_ROWS; r++) acc[r] = floatx16{0};
@@ -656,8 +727,10 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
             const int ncb = (cb + 1) & (XP_NCB - 1);
             if (mfma_wave) {
                 xp_cblock<F16>(acc, an, wf, mt, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
-            } else if (ntile < ntiles) {
-                xp_fill<FIRST, IN_CB, F16>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, tiles_x, ncb, st, s);
+            } else if (ntile < bt.ntiles) {
+                float sn, un;
+                scales(ntile, sn, un);
+                xp_fill<FIRST, IN_CB, F16>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, bt, ncb, st, sn, win);
             }
             if (cb == XP_NCB - 1) {
                 // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
@@ -669,8 +742,11 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                 float bv[16];
 #pragma unroll
                 for (int i = 0; i < 16; i++) bv[i] = bias[mt * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+                float amax = 0.0f;   // F16, !LAST: max of this wave's stored outputs of the tile
                 if (F16 && mfma_wave) {
                     // undo the power-of-two scalings (exact)
+                    float s_unused, unscale;
+                    scales(tile, s_unused, unscale);
 #pragma unroll
                     for (int r = 0; r < XP_ROWS; r++)
 #pragma unroll
@@ -690,11 +766,18 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                                                                  fmaxf(acc[r][4 * q + 3] + bv[4 * q + 3], 0.f));
                                     if (F16) amax = fmaxf(amax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
                                     const int c = mt * 32 + 8 * q + 4 * h;
-                                    float *dst = OUT_CB ? out + (((size_t)(c >> 4) * Hout + y) * Wout + x) * 16 + (c & 15)
-                                                        : out + ((size_t)y * Wout + x) * NF + c;
+                                    float *dst = OUT_CB ? outi + (((size_t)(c >> 4) * Hout + y) * Wout + x) * 16 + (c & 15)
+                                                        : outi + ((size_t)y * Wout + x) * NF + c;
                                     if (!(TOWER_DIAG & 16) || o.x == -1.0f) *reinterpret_cast<float4 *>(dst) = o;
                                 }
                             }
+                        }
+                        if (F16) {   // outputs are >= +0 (ReLU): their float bits order like their values
+#pragma unroll
+                            for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+                            if (lane == 0)
+                                atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride),
+                                          __float_as_uint(amax));
                         }
                     }
                 } else {
@@ -728,11 +811,11 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                             if (h == 0) red1[(mt * XP_TY + row) * XP_TX + j] = s2;
                             const int y = ty0 + row, x = tx0 + j;
                             if (y < Hout && x < Wout) {
-                                const size_t pix = (size_t)y * Wout + x;
+                                const size_t pix = (size_t)y * Wout + x + img * bt.pix_stride;
 #pragma unroll
                                 for (int q = 0; q < 4; q++) {
                                     const int c = mt * 32 + 8 * q + 4 * h;
-                                    *reinterpret_cast<float4 *>(out + pix * NF + c) =
+                                    *reinterpret_cast<float4 *>(out + pix * NF + c) =   // pix includes the image
                                         make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
                                     if (ohi) {
                                         bf16x4 hv, lv;
@@ -756,7 +839,7 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                         for (int r = 0; r < XP_ROWS; r++) {
                             const int row = XP_ROWS * g + r, y = ty0 + row, x = tx0 + j;
                             if (y < Hout && x < Wout)   // fp32 rounding bound of the 64-term sum
-                                onrm[(size_t)y * Wout + x] =
+                                onrm[(size_t)y * Wout + x + img * bt.pix_stride] =
                                     sqrtf(red1[row * XP_TX + j] + red1[(XP_TY + row) * XP_TX + j]) * 1.000004f;
                         }
                     }
@@ -770,12 +853,6 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         out[2 * blockIdx.x] = (float)(t1 - t_start);
         out[2 * blockIdx.x + 1] = (float)(r1 - r_start);
-    }
-    if (F16 && !LAST && mfma_wave) {
-        // outputs are >= +0 (ReLU): their float bits order like their values
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax), __float_as_uint(amax));
     }
 }
 
@@ -979,13 +1056,19 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
     return SDE_OK;
 }
 
+SDE_EXPORT int64_t sde_tower_batch_workspace_bytes(int H, int W, int nimg, int nlayers, int nf)
+{
+    if (H <= 0 || W <= 0 || nimg <= 0 || nlayers < 1 || nf != NF) return -1;
+    if (nlayers == 1) return 0;
+    // two ping-pong activation buffers sized for layer 2's output (nimg images each), then the
+    // F16X3 bound words (64 per image)
+    const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
+    return (nlayers > 2 ? 2 * nimg * h2 * w2 * NF * (int64_t)sizeof(float) : 0) + nimg * TOWER_AMAX_BYTES;
+}
+
 SDE_EXPORT int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf)
 {
-    if (H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return -1;
-    if (nlayers == 1) return 0;
-    // two ping-pong activation buffers sized for layer 2's output, then the F16X3 bound words
-    const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
-    return (nlayers > 2 ? 2 * h2 * w2 * NF * (int64_t)sizeof(float) : 0) + TOWER_AMAX_BYTES;
+    return sde_tower_batch_workspace_bytes(H, W, 1, nlayers, nf);
 }
 
 static void set_tower_attrs()
@@ -1031,9 +1114,12 @@ static int cu_count()
 // in_cb / out_cb: activations in the c-block-major layout [4][h][w][16] (bf16x6 / f16x3 paths).
 // F16X3: in_amax = bound of |input| (|image| for layer 2), out_amax = max of the ReLU outputs
 // (zeroed by the caller; unused by the last layer).
+// nimg images per launch (split arithmetics: one tile space over the batch; fp32: one launch per
+// image): image i at in + i * in_stride, out + i * out_stride, bound words + i * amax_stride.
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
                          int flags, uint16_t *ohi, uint16_t *olo, float *onrm, bool in_cb, bool out_cb,
-                         const float *in_amax, float *out_amax, hipStream_t st)
+                         const float *in_amax, float *out_amax, hipStream_t st, int nimg = 1, int64_t in_stride = 0,
+                         int64_t out_stride = 0, int amax_stride = 0)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
@@ -1043,11 +1129,18 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
     if (x6) {
-        const int tiles_x = cdiv(wout, XP_TX), ntiles = tiles_x * cdiv(hout, XP_TY);
-        const int grid = std::min(ntiles, cu_count());
+        XpBatch bt;
+        bt.tiles_x = cdiv(wout, XP_TX);
+        bt.tiles_img = bt.tiles_x * cdiv(hout, XP_TY);
+        bt.ntiles = bt.tiles_img * nimg;
+        bt.in_stride = in_stride;
+        bt.out_stride = out_stride;
+        bt.pix_stride = (int64_t)hout * wout;
+        bt.amax_stride = amax_stride;
+        const int grid = std::min(bt.ntiles, cu_count());
 #define SDE_X6P(F, L, I, O, H) conv64_x6p_kernel<F, L, I, O, H><<<grid, 512, XP_SMEM, st>>>( \
         in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
-        (L) ? onrm : nullptr, tiles_x, ntiles, in_amax, out_amax)
+        (L) ? onrm : nullptr, bt, in_amax, out_amax)
 #define SDE_X6P_ALL(H)                                                      \
         if (layer == 2) {                                                   \
             if (last) SDE_X6P(true, true, false, false, H);                 \
@@ -1068,11 +1161,18 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         return;
     }
     dim3 grid(cdiv(wout, TW_TX), cdiv(hout, TW_TY));
-#define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, \
-                                                             (L) ? ohi : nullptr, (L) ? olo : nullptr, (L) ? onrm : nullptr)
-    if (layer == 2) { if (last) SDE_CONV(conv64_mfma_kernel, true, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, true, false, TW_SMEM); }
-    else { if (last) SDE_CONV(conv64_mfma_kernel, false, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, false, false, TW_SMEM); }
+    const int64_t pix = (int64_t)hout * wout;
+    for (int i = 0; i < nimg; i++) {
+        const float *ini = in + i * in_stride;
+        float *outi = out + i * out_stride;
+        uint16_t *hi = ohi ? ohi + i * pix * NF : nullptr, *lo = olo ? olo + i * pix * NF : nullptr;
+        float *nr = onrm ? onrm + i * pix : nullptr;
+#define SDE_CONV(K, F, L, SM) K<F, L><<<grid, 512, SM, st>>>(ini, Hin, Win, (F) ? w1 : nullptr, wk, outi, hout, wout, \
+                                                             (L) ? hi : nullptr, (L) ? lo : nullptr, (L) ? nr : nullptr)
+        if (layer == 2) { if (last) SDE_CONV(conv64_mfma_kernel, true, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, true, false, TW_SMEM); }
+        else { if (last) SDE_CONV(conv64_mfma_kernel, false, true, TW_SMEM); else SDE_CONV(conv64_mfma_kernel, false, false, TW_SMEM); }
 #undef SDE_CONV
+    }
 }
 
 static bool tower_flags_ok(int flags, bool layer_api)
@@ -1101,6 +1201,27 @@ SDE_EXPORT int sde_tower_layer_scaled(const float *in, int Hin, int Win, const f
     return launch_status();
 }
 
+SDE_EXPORT int sde_tower_layer_batch(const float *in, int nimg, int64_t in_stride, int Hin, int Win,
+                                     const float *packed, int nlayers, int nf, int layer, float *out,
+                                     int64_t out_stride, int flags, const float *in_absmax, float *out_absmax,
+                                     int amax_stride, void *stream)
+{
+    if (!in || !packed || !out || nf != NF || nlayers < 2 || layer < 2 || layer > nlayers || nimg <= 0) return SDE_ERR_ARG;
+    if (Hin < (layer == 2 ? 5 : 3) || Win < (layer == 2 ? 5 : 3)) return SDE_ERR_ARG;
+    if (!tower_flags_ok(flags, true)) return SDE_ERR_ARG;
+    const bool in_cb = (flags & SDE_TOWER_IN_CBLOCK) != 0, out_cb = (flags & SDE_TOWER_OUT_CBLOCK) != 0;
+    if ((in_cb && layer == 2) || (out_cb && layer == nlayers)) return SDE_ERR_ARG;
+    const int64_t hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
+    const int64_t in_need = layer == 2 ? (int64_t)Hin * Win : (int64_t)Hin * Win * NF;
+    if (nimg > 1 && (in_stride < in_need || out_stride < hout * wout * NF ||
+                     (layer == nlayers && out_stride != hout * wout * NF))) return SDE_ERR_ARG;
+    if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax) || (nimg > 1 && amax_stride < 1)))
+        return SDE_ERR_ARG;
+    launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, nullptr, nullptr, nullptr, in_cb, out_cb,
+                 in_absmax, out_absmax, as_stream(stream), nimg, in_stride, out_stride, amax_stride);
+    return launch_status();
+}
+
 SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int nf, int layer,
                                float *out, int flags, uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm,
                                void *stream)
@@ -1120,52 +1241,70 @@ SDE_EXPORT int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *st
     return launch_status();
 }
 
-SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
-                                 float *feat, void *workspace, int64_t workspace_bytes, int flags, uint16_t *feat_hi,
-                                 uint16_t *feat_lo, float *feat_norm, void *stream)
+SDE_EXPORT int sde_tower_forward_batch(const float *img_pad, int nimg, int H, int W, const float *packed, int nlayers,
+                                       int nf, float *feat, void *workspace, int64_t workspace_bytes, int flags,
+                                       uint16_t *feat_hi, uint16_t *feat_lo, float *feat_norm, void *stream)
 {
     if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
     if (nlayers == 1 && (feat_hi || feat_norm)) return SDE_ERR_ARG;
-    if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
+    if (!img_pad || !packed || !feat || H <= 0 || W <= 0 || nimg <= 0 || nlayers < 1 || nf != NF) return SDE_ERR_ARG;
     if (!tower_flags_ok(flags, false)) return SDE_ERR_ARG;
-    const int64_t need = sde_tower_workspace_bytes(H, W, nlayers, nf);
+    const int64_t need = sde_tower_batch_workspace_bytes(H, W, nimg, nlayers, nf);
     if (need > 0 && (!workspace || workspace_bytes < need)) return SDE_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
     const int Hp = H + 2 * nlayers, Wp = W + 2 * nlayers;
+    const int64_t img_stride = (int64_t)Hp * Wp, feat_stride = (int64_t)H * W * NF;
     if (nlayers == 1) {
-        conv1_only_kernel<<<cdiv((int64_t)H * W, 256), 256, 0, st>>>(img_pad, Hp, Wp, packed, feat);
+        for (int i = 0; i < nimg; i++)
+            conv1_only_kernel<<<cdiv((int64_t)H * W, 256), 256, 0, st>>>(img_pad + i * img_stride, Hp, Wp, packed,
+                                                                         feat + i * feat_stride);
         return launch_status();
     }
     float *buf[2] = {nullptr, nullptr};
     const int64_t h2 = H + 2 * (nlayers - 2), w2 = W + 2 * (nlayers - 2);
+    const int64_t act_stride = h2 * w2 * NF;   // per image, sized for layer 2's output
     if (nlayers > 2) {
         buf[0] = reinterpret_cast<float *>(workspace);
-        buf[1] = buf[0] + h2 * w2 * NF;
+        buf[1] = buf[0] + nimg * act_stride;
     }
-    // F16X3 bound words: amax[l - 2] bounds |input of layer l|
-    float *amax = reinterpret_cast<float *>(static_cast<char *>(workspace) + (nlayers > 2 ? 2 * h2 * w2 * NF * 4 : 0));
+    // F16X3 bound words: amax[i * 64 + l - 2] bounds |input of layer l| of image i
+    float *amax = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                            (nlayers > 2 ? 2 * nimg * act_stride * 4 : 0));
+    constexpr int AS = (int)(TOWER_AMAX_BYTES / 4);
     const bool f16 = (flags & SDE_TOWER_F16X3) != 0;
     if (f16) {
-        if (nlayers > (int)(TOWER_AMAX_BYTES / 4)) return SDE_ERR_ARG;
-        if (hipMemsetAsync(amax, 0, TOWER_AMAX_BYTES, st) != hipSuccess) return SDE_ERR_LAUNCH;
-        const int rc = sde_absmax_f32(img_pad, (int64_t)Hp * Wp, amax, stream);
-        if (rc != SDE_OK) return rc;
+        if (nlayers > AS) return SDE_ERR_ARG;
+        if (hipMemsetAsync(amax, 0, nimg * TOWER_AMAX_BYTES, st) != hipSuccess) return SDE_ERR_LAUNCH;
+        for (int i = 0; i < nimg; i++) {
+            const int rc = sde_absmax_f32(img_pad + i * img_stride, img_stride, amax + i * AS, stream);
+            if (rc != SDE_OK) return rc;
+        }
     }
     int hin = Hp, win = Wp;
     // intermediate activations in the c-block-major layout on the split paths
     const bool cbl = (flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) != 0;
     launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, feat_hi, feat_lo, feat_norm,
-                 false, cbl && nlayers > 2, amax, amax + 1, st);
+                 false, cbl && nlayers > 2, amax, amax + 1, st, nimg, img_stride,
+                 nlayers == 2 ? feat_stride : act_stride, AS);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
         launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, cbl,
-                     cbl && l < nlayers, amax + (l - 2), amax + (l - 1), st);
+                     cbl && l < nlayers, amax + (l - 2), amax + (l - 1), st, nimg, act_stride,
+                     l == nlayers ? feat_stride : act_stride, AS);
         hin -= 2; win -= 2;
         cur ^= 1;
     }
     return launch_status();
+}
+
+SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float *packed, int nlayers, int nf,
+                                 float *feat, void *workspace, int64_t workspace_bytes, int flags, uint16_t *feat_hi,
+                                 uint16_t *feat_lo, float *feat_norm, void *stream)
+{
+    return sde_tower_forward_batch(img_pad, 1, H, W, packed, nlayers, nf, feat, workspace, workspace_bytes, flags,
+                                   feat_hi, feat_lo, feat_norm, stream);
 }
 
 SDE_EXPORT int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,

@@ -278,6 +278,33 @@ def absmax(x, out):
     return out
 
 
+def tower_batch_workspace_bytes(H: int, W: int, nimg: int, nlayers: int, nf: int = 64) -> int:
+    return int(lib.sde_tower_batch_workspace_bytes(H, W, nimg, nlayers, nf))
+
+
+def tower_forward_batch(img_pad, packed, nlayers: int, nf: int = 64, out=None, workspace=None,
+                        precision: str = "f16x3"):
+    """img_pad: f32 [N, H+2L, W+2L] -> features f32 [N, H, W, nf], all N images per launch
+    (sde_tower_forward_batch); each image's result equals tower_forward on it alone."""
+    N, Hp, Wp = img_pad.shape
+    H, W = Hp - 2 * nlayers, Wp - 2 * nlayers
+    if H <= 0 or W <= 0:
+        raise ValueError("padded image smaller than the tower's receptive field")
+    pi = _need(img_pad, "img_pad")
+    pw = _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),))
+    if out is None:
+        out = _empty((N, H, W, nf), torch.float32, img_pad)
+    po = _need(out, "features", shape=(N, H, W, nf))
+    need = tower_batch_workspace_bytes(H, W, N, nlayers, nf)
+    if need > 0 and workspace is None:
+        workspace = torch.empty(need, dtype=torch.uint8, device=img_pad.device)
+    pws = _need(workspace, "workspace", dtype=torch.uint8) if need > 0 else None
+    wsb = workspace.numel() if need > 0 else 0
+    check(lib.sde_tower_forward_batch(pi, N, H, W, pw, nlayers, nf, po, pws, wsb, TOWER_PRECISIONS[precision],
+                                      None, None, None, _stream()), "sde_tower_forward_batch")
+    return out
+
+
 def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
                 in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
     """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
@@ -304,6 +331,33 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precis
                                      nlayers, nf, layer, _need(out, "layer output", shape=oshape),
                                      flags, *_split_ptrs(split, oshape[:2]), pin, pout, _stream()),
           "sde_tower_layer_scaled")
+    return out
+
+
+def tower_layer_batch(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "f16x3",
+                      in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
+    """tower_layer over a batch per launch: inp [N, Hin, Win] (layer 2) or [N, Hin, Win, nf], out
+    [N, h, w, nf]; in_absmax / out_absmax (f16x3): [N, k] device words, column 0 used (row stride k)."""
+    flags = TOWER_PRECISIONS[precision]
+    if in_cblock:
+        flags |= _lib.SDE_TOWER_IN_CBLOCK
+    if out_cblock:
+        flags |= _lib.SDE_TOWER_OUT_CBLOCK
+    N, Hin, Win = inp.shape[:3]
+    sh = 4 if layer == 2 else 2
+    oshape = (N, Hin - sh, Win - sh, nf)
+    ws = 0
+    pin = pout = None
+    if in_absmax is not None:
+        pin, ws = in_absmax.data_ptr(), in_absmax.stride(0)
+    if out_absmax is not None:
+        pout = out_absmax.data_ptr()
+    _need(inp, "layer input")
+    _need(out, "layer output", shape=oshape)
+    check(lib.sde_tower_layer_batch(inp.data_ptr(), N, inp[0].numel(), Hin, Win,
+                                    _need(packed, "packed weights", shape=(tower_packed_floats(nlayers, nf),)),
+                                    nlayers, nf, layer, out.data_ptr(), out[0].numel(), flags, pin, pout, ws,
+                                    _stream()), "sde_tower_layer_batch")
     return out
 
 

@@ -43,10 +43,13 @@ class StereoMatcher:
         H, W, L = self.H, self.W, self.nlayers
         self.packed = torch.from_numpy(packed).to(dev)
         self.img_u8 = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.img_pad = [torch.empty((H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev) for _ in range(2)]
+        # both images in one allocation: the tower runs the pair per launch (sde_tower_forward_batch)
+        self.img_pad2 = torch.empty((2, H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev)
+        self.img_pad = [self.img_pad2[0], self.img_pad2[1]]
         self.stats = [torch.empty((ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.feat = [torch.empty((H, W, nf), dtype=torch.float32, device=dev) for _ in range(2)]
-        nws = ops.tower_workspace_bytes(H, W, L, nf)
+        self.feat2 = torch.empty((2, H, W, nf), dtype=torch.float32, device=dev)
+        self.feat = [self.feat2[0], self.feat2[1]]
+        nws = ops.tower_batch_workspace_bytes(H, W, 2, L, nf)
         self.ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
         self.min_cost = torch.empty((H, W), dtype=torch.float32, device=dev)
@@ -74,16 +77,17 @@ class StereoMatcher:
         """Preprocess + tower for both images (compute_feature, process_functional.py:11-45)."""
         for i in range(2):
             ops.preprocess_u8(self.img_u8[i], self.nlayers, out=self.img_pad[i], stats=self.stats[i])
-            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
-                              precision=self.tower_precision, split=self.split[i] if self.split else None)
-        self.split_valid = self.split is not None
-        return self.feat[0], self.feat[1]
+        return self.features_from_padded()
 
     def features_from_padded(self):
-        """Tower only, on already-normalised padded images in self.img_pad."""
-        for i in range(2):
-            ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i], workspace=self.ws,
-                              precision=self.tower_precision, split=self.split[i] if self.split else None)
+        """Tower only, on already-normalised padded images in self.img_pad (the pair per launch)."""
+        if self.split:
+            for i in range(2):
+                ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i],
+                                  workspace=self.ws, precision=self.tower_precision, split=self.split[i])
+        else:
+            ops.tower_forward_batch(self.img_pad2, self.packed, self.nlayers, self.nf, out=self.feat2,
+                                    workspace=self.ws, precision=self.tower_precision)
         self.split_valid = self.split is not None
         return self.feat[0], self.feat[1]
 

@@ -638,3 +638,37 @@ def test_absmax(gpu, off, n):
     ops.absmax(xd, word)
     want = max(1.5, float(np.abs(x[off:]).max())) if n else 1.5
     assert float(word.cpu()[0]) == want
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("nlayers,H,W,N", [(5, 150, 300, 2), (3, 70, 45, 3), (2, 33, 90, 2), (1, 9, 12, 2),
+                                           (5, 40, 33, 1)])
+def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
+    """sde_tower_forward_batch (all images in one persistent tile space, per-image bound words)
+    gives every image exactly what sde_tower_forward gives it alone; the layer-by-layer batch API
+    chained the same way gives the same bits."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    rng = np.random.default_rng(N * 100 + H)
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(nlayers, seed=4), nlayers)))
+    L = nlayers
+    imgs = torch.zeros((N, H + 2 * L, W + 2 * L), device="cuda")
+    for i in range(N):   # images of very different dynamic range: per-image f16x3 scalings
+        imgs[i, L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32) * 10.0 ** (2 * i)).cuda()
+    out = ops.tower_forward_batch(imgs, packed, L, precision=precision)
+    for i in range(N):
+        single = ops.tower_forward(imgs[i].contiguous(), packed, L, precision=precision)
+        assert torch.equal(out[i], single), (precision, i)
+    if L >= 2:
+        cbl = precision != "fp32"
+        words = torch.zeros((N, 8), device="cuda")
+        for i in range(N):
+            ops.absmax(imgs[i], words[i, 0:1])
+        x = imgs
+        for layer in range(2, L + 1):
+            sh = 4 if layer == 2 else 2
+            y = torch.empty((N, x.shape[1] - sh, x.shape[2] - sh, 64), device="cuda")
+            ops.tower_layer_batch(x, packed, L, layer, y, precision=precision, in_cblock=cbl and layer > 2,
+                                  out_cblock=cbl and layer < L, in_absmax=words[:, layer - 2:layer - 1],
+                                  out_absmax=words[:, layer - 1:layer] if layer < L else None)
+            x = y
+        assert torch.equal(x, out)
