@@ -316,11 +316,20 @@ constexpr int XP_STAGE = 6 * XP_PLANE;            // one c-block stage: 58,752 B
 constexpr int XP_UNITS = XP_NPIX * 4;             // (pixel, 4-channel chunk) units per stage
 constexpr int XP_STAGERS = 256;                   // threads of the stager waves
 constexpr int XP_UPT = (XP_UNITS + XP_STAGERS - 1) / XP_STAGERS;   // units per stager thread (10)
-constexpr int XP_ROWS = 8;                        // output rows per MFMA wave
-constexpr int XP_RED = 2 * 2 * XP_TY * XP_TX * 4; // LAST: two per-M-tile partial-sum exchanges
+// MFMA wave mapping: WR output rows x 64 / (8 / WR)... per wave -- WR = 8: one M-tile (32 output
+// channels) of 8 rows; WR = 4: both M-tiles of 4 rows (a pixel's 64 channels in one wave, as the
+// last layer's L2 norm wants).  8 accumulators either way.
+#ifndef XP_WR_MID
+#define XP_WR_MID 4
+#endif
+#ifndef XP_WR_FIRST
+#define XP_WR_FIRST 4
+#endif
+constexpr int XP_ACC = 8;                         // accumulators per MFMA wave
+#define XP_AL(F16, WR) (((WR) == 8 || (F16)) ? 2 : 1)   // A fragments requested this many taps ahead
 constexpr int XP_WX = XP_IX + 2, XP_WIN = (XP_IY + 2) * XP_WX;   // FIRST: image window of a tile (20 x 36)
-// two stages | LAST's partial-sum exchanges | FIRST: one image window per stager wave
-constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + XP_RED + 4 * XP_WIN * sizeof(float);
+// two stages | FIRST: one image window per stager wave
+constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + 4 * XP_WIN * sizeof(float);
 constexpr int XP_NCB = NF / 16;                   // c-blocks per pixel
 
 // Split 4 channels and store them into the stage's six planes.
@@ -505,14 +514,36 @@ __device__ __forceinline__ void xp_scales(bool first, const float *__restrict__ 
 // Stager waves' own loop (non-FIRST layers): the pipeline of (tile, c-block) steps the MFMA
 // waves consume, one stage ahead, with the HBM loads of step i+2 issued before step i+1's
 // units are split and stored -- every load has a whole c-block period to land.  Runs the
-// same barriers as the MFMA waves: one per c-block, plus LAST's two per tile.
-template <bool IN_CB, bool LAST, bool F16>
+// same barriers as the MFMA waves: one per c-block.
+template <bool FIRST, bool IN_CB, bool F16>
 __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restrict__ in, int Hin, int Win,
                                                const XpBatch &bt, int st, const float *__restrict__ in_amax,
-                                               const float *__restrict__ hdr)
+                                               const float *__restrict__ hdr, const float *__restrict__ w1blob,
+                                               float *win)
 {
     const int tile0 = blockIdx.x, gstride = gridDim.x;
     const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * XP_NCB;
+    if (FIRST) {
+        // conv1 on the stagers: each step computed from the wave's LDS image window, one stage ahead
+        int sc_img = -1;
+        float s = 1.0f, unscale = 1.0f;
+        auto fill = [&](int i) {
+            const int t = tile0 + (i / XP_NCB) * gstride, im = t / bt.tiles_img;
+            if (F16 && im != sc_img) {
+                xp_scales(true, in_amax + im * bt.amax_stride, hdr, s, unscale);
+                sc_img = im;
+            }
+            xp_fill<true, false, F16>(xsm + (i & 1) * XP_STAGE, in, Hin, Win, w1blob, t, bt, i % XP_NCB, st, s, win);
+        };
+        fill(0);
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < nsteps; i++) {
+            if (i + 1 < nsteps) fill(i + 1);
+            if (!(TOWER_DIAG & 32)) __syncthreads();
+        }
+        return;
+    }
     auto load = [&](float4 (&v)[XP_UPT], int i) {
         const int t = tile0 + (i / XP_NCB) * gstride, cb = i % XP_NCB;
         int img, ty0, tx0;
@@ -541,8 +572,7 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
             if (u < XP_UNITS) xp_store<F16>(sb, u, v[k], s);
         }
     };
-    auto sync_step = [&](int i) {
-        if (LAST && i % XP_NCB == XP_NCB - 1) { __syncthreads(); __syncthreads(); }
+    auto sync_step = [&](int) {
         if (!(TOWER_DIAG & 32)) __syncthreads();
     };
     float4 ra[XP_UPT], rb[XP_UPT];
@@ -600,52 +630,74 @@ __device__ __forceinline__ floatx16 mfma_h(bf16x8 a, bf16x8 b, floatx16 c)
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
-// One c-block for one MFMA wave: 9 taps x 8 rows = 72 row-steps of 6 MFMAs (small terms
-// first, the leading product last).  B fragments are read two row-steps ahead (a 3-deep
-// register ring) and sched_barrier fences keep the scheduler from hoisting more, which
-// bounds the live registers (8 accumulators = 128 of the 256 a wave may hold at 2 waves
-// per SIMD).  A fragments for tap t+1 are requested when tap t starts.  Rows past the
-// output edge run on zero-filled input and are discarded by the epilogue.
-template <bool F16>
-__device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ROWS], XpFrag (&an)[2], const uint4 *__restrict__ wf,
-                                          int mt, int cb, int ncb, int lane, const char *sb)
+// One c-block for one MFMA wave: 9 taps x 4 output rows = 36 row-steps; each step's B
+// fragment (one input row segment, NP parts) feeds both M-tiles (output channels 0-31 and
+// 32-63): 2 x 6 (bf16x6) or 2 x 3 (F16) MFMAs, small terms first, the leading product last.
+// B fragments are read RD-1 row-steps ahead (a register ring); sched_barrier fences keep the
+// scheduler from hoisting more, which bounds the live registers (8 accumulators = 128 of the
+// 256 a wave may hold at 2 waves per SIMD).  A fragments (both M-tiles) are requested AL taps
+// ahead.  Rows past the output edge run on zero-filled input and are discarded by the epilogue.
+template <bool F16, int WR>
+__device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8 / WR],
+                                          XpFrag (&an)[XP_AL(F16, WR)][8 / WR], const uint4 *__restrict__ wf, int mt0,
+                                          int cb, int ncb, int lane, const char *sb)
 {
-    constexpr int NS = 9 * XP_ROWS;
+    constexpr int XP_WROWS = WR, MW = 8 / WR;
+    constexpr int NS = 9 * XP_WROWS;
     constexpr int NP = F16 ? 2 : 3;
+    constexpr int AL = XP_AL(F16, WR);
     constexpr int RD = F16 ? XP_RING_F16 : 3;   // ring depth: fragments read RD-1 row-steps ahead
     XpB ring[RD];
-    auto boff = [&](int s) { return ((s / XP_ROWS / 3 + s % XP_ROWS) * XP_IX + (s / XP_ROWS) % 3) * 16; };
+    auto boff = [&](int s) { return ((s / XP_WROWS / 3 + s % XP_WROWS) * XP_IX + (s / XP_WROWS) % 3) * 16; };
 #pragma unroll
     for (int k = 0; k < RD - 1; k++) ring[k] = xp_bfrag<NP>(sb + boff(k));
-    XpFrag a = an[0];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-        const int tap = s / XP_ROWS, r = s % XP_ROWS;
-        if (r == 0) {
-            // A fragments two taps ahead: an[0] = A(tap + 1), an[1] = A(tap + 2)
-            if (tap > 0) a = an[0];
-            an[0] = an[1];
-            if (TOWER_DIAG & 64) an[1] = an[0];
-            else an[1] = tap < 7 ? xp_afrag<NP>(wf, mt, cb, tap + 2, lane) : xp_afrag<NP>(wf, mt, ncb, tap - 7, lane);
+        const int tap = s / XP_WROWS, r = s % XP_WROWS;
+        if (r == 0 && tap > 0) {
+            // a = A(tap); an[k] = A(tap + 1 + k); request A(tap + AL) (the next c-block's past tap 8)
+#pragma unroll
+            for (int m = 0; m < MW; m++) {
+                a[m] = an[0][m];
+#pragma unroll
+                for (int k = 0; k + 1 < AL; k++) an[k][m] = an[k + 1][m];
+                const int t2 = tap + AL;
+                if (TOWER_DIAG & 64) an[AL - 1][m] = a[m];
+                else an[AL - 1][m] = t2 < 9 ? xp_afrag<NP>(wf, mt0 + m, cb, t2, lane)
+                                            : xp_afrag<NP>(wf, mt0 + m, ncb, t2 - 9, lane);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         const XpB &b = ring[s % RD];
-        if (TOWER_DIAG & 4) {
 #pragma unroll
-            for (int q = 0; q < NP; q++) asm volatile("" ::"v"(b.p[q]), "v"(a.p[q]));   // keep the fragments live
-        } else if (F16) {
-            acc[r] = mfma_h(a.p[1], b.p[0], acc[r]);
-            acc[r] = mfma_h(a.p[0], b.p[1], acc[r]);
-            acc[r] = mfma_h(a.p[0], b.p[0], acc[r]);
-        } else {
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc[r], 0, 0, 0);
+        for (int m = 0; m < MW; m++) {
+            floatx16 &c = acc[m * XP_WROWS + r];
+            if (TOWER_DIAG & 4) {
+#pragma unroll
+                for (int q = 0; q < NP; q++) asm volatile("" ::"v"(b.p[q]), "v"(a[m].p[q]));   // keep the fragments live
+            } else if (F16) {
+                c = mfma_h(a[m].p[1], b.p[0], c);
+                c = mfma_h(a[m].p[0], b.p[1], c);
+                c = mfma_h(a[m].p[0], b.p[0], c);
+            } else {
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[2], b.p[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[1], b.p[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[0], b.p[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[1], b.p[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[0], b.p[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m].p[0], b.p[0], c, 0, 0, 0);
+            }
         }
         if (s + RD - 1 < NS) ring[(s + RD - 1) % RD] = xp_bfrag<NP>(sb + boff(s + RD - 1));
+    }
+    // hand the c-block boundary over: a = A(next c-block, tap 0)
+#pragma unroll
+    for (int m = 0; m < MW; m++) {
+        a[m] = an[0][m];
+#pragma unroll
+        for (int k = 0; k + 1 < AL; k++) an[k][m] = an[k + 1][m];
+        if (TOWER_DIAG & 64) an[AL - 1][m] = a[m];
+        else an[AL - 1][m] = xp_afrag<NP>(wf, mt0 + m, ncb, AL, lane);
     }
 }
 
@@ -659,22 +711,25 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                                                          const float *__restrict__ in_amax, float *__restrict__ out_amax)
 {
     extern __shared__ __attribute__((aligned(16))) char xsm[];
-    float *red0 = reinterpret_cast<float *>(xsm + 2 * XP_STAGE);   // [2 mt][16 rows][32 px]
-    float *red1 = red0 + 2 * XP_TY * XP_TX;
     // FIRST: the stager wave's image window
-    float *win = reinterpret_cast<float *>(xsm + 2 * XP_STAGE + XP_RED) + ((threadIdx.x >> 6) & 3) * XP_WIN;
+    float *win = reinterpret_cast<float *>(xsm + 2 * XP_STAGE) + ((threadIdx.x >> 6) & 3) * XP_WIN;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const bool mfma_wave = wave < 4;            // waves 4..7 stage the input
-    const int mt = wave & 1, g = (wave >> 1) & 1;
+    constexpr int XP_WROWS = LAST ? 4 : (FIRST ? XP_WR_FIRST : XP_WR_MID), MW = 8 / XP_WROWS;
+    static_assert(XP_WROWS == 4 || XP_WROWS == 8, "wave mapping");
+    // MFMA wave: output rows XP_WROWS*g .. +XP_WROWS-1, M-tiles mt0 .. mt0+MW-1
+    const int g = XP_WROWS == 4 ? (wave & 3) : ((wave >> 1) & 1);
+    const int mt0 = XP_WROWS == 4 ? 0 : (wave & 1);
     const int st = tid - XP_STAGERS;            // stager thread index (valid when !mfma_wave)
     constexpr int NP = F16 ? 2 : 3;
+    constexpr int AL = XP_AL(F16, XP_WROWS);
     const float *bias = wkblob;
     const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + (F16 ? LK_F16 : NF + LK_W));
-    // B fragment: plane (part, h), input row 8g + r + ky, pixel j + kx
-    const int bbase = (lane >> 5) * XP_PLANE + ((XP_ROWS * g) * XP_IX + (lane & 31)) * 16;
+    // B fragment: plane (part, h), input row XP_WROWS*g + r + ky, pixel j + kx
+    const int bbase = (lane >> 5) * XP_PLANE + ((XP_WROWS * g) * XP_IX + (lane & 31)) * 16;
 
     int tile = blockIdx.x;
     if (tile >= bt.ntiles) return;
@@ -696,19 +751,16 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         sc = sc_s;
         usc = sc_u;
     };
-    if (!FIRST && !LAST && !mfma_wave) {
-        xp_stager_loop<IN_CB, LAST, F16>(xsm, in, Hin, Win, bt, st, in_amax, hdr);
+    if (!mfma_wave) {
+        xp_stager_loop<FIRST, IN_CB, F16>(xsm, in, Hin, Win, bt, st, in_amax, hdr, w1blob, win);
         return;
     }
-    XpFrag an[2];
-    if (mfma_wave) {
-        an[0] = xp_afrag<NP>(wf, mt, 0, 0, lane);
-        an[1] = xp_afrag<NP>(wf, mt, 0, 1, lane);
-    }
-    else {
-        float s0, u0;
-        scales(tile, s0, u0);
-        xp_fill<FIRST, IN_CB, F16>(xsm, in, Hin, Win, w1blob, tile, bt, 0, st, s0, win);
+    XpFrag a[MW], an[AL][MW];
+#pragma unroll
+    for (int m = 0; m < MW; m++) {
+        a[m] = xp_afrag<NP>(wf, mt0 + m, 0, 0, lane);
+#pragma unroll
+        for (int k = 0; k < AL; k++) an[k][m] = xp_afrag<NP>(wf, mt0 + m, 0, 1 + k, lane);
     }
     __syncthreads();
 
@@ -716,131 +768,112 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     for (; tile < bt.ntiles; tile += gridDim.x) {
         int img, ty0, tx0;
         xp_tile(bt, tile, img, ty0, tx0);
-        float *const outi = out + img * bt.out_stride;
-        floatx16 acc[XP_ROWS];
+        floatx16 acc[XP_ACC];
 #pragma unroll
-        for (int r = 0; r < XP_ROWS; r++) acc[r] = floatx16{0};
+        for (int r = 0; r < XP_ACC; r++) acc[r] = floatx16{0};
 
 #pragma unroll 1
         for (int cb = 0; cb < XP_NCB; cb++) {
-            const int ntile = cb + 1 < XP_NCB ? tile : tile + (int)gridDim.x;
             const int ncb = (cb + 1) & (XP_NCB - 1);
-            if (mfma_wave) {
-                xp_cblock<F16>(acc, an, wf, mt, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
-            } else if (ntile < bt.ntiles) {
-                float sn, un;
-                scales(ntile, sn, un);
-                xp_fill<FIRST, IN_CB, F16>(xsm + (cur ^ 1) * XP_STAGE, in, Hin, Win, w1blob, ntile, bt, ncb, st, sn, win);
-            }
+            xp_cblock<F16, XP_WROWS>(acc, a, an, wf, mt0, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
             if (cb == XP_NCB - 1) {
                 // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
-                // lane holds pixel column j, channels mt*32 + 8q + 4h + e in acc[r][4q + e]
+                // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
                 // opaque copies of the lane coordinates: keep the epilogue's bias loads and
                 // addresses inside the loop (hoisted, they would pin registers for the whole kernel)
                 int j = lane & 31, h = lane >> 5;
                 asm volatile("" : "+v"(j), "+v"(h));
-                float bv[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) bv[i] = bias[mt * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
-                float amax = 0.0f;   // F16, !LAST: max of this wave's stored outputs of the tile
-                if (F16 && mfma_wave) {
-                    // undo the power-of-two scalings (exact)
-                    float s_unused, unscale;
+                float unscale = 1.0f;
+                if (F16) {   // undo the power-of-two scalings (exact)
+                    float s_unused;
                     scales(tile, s_unused, unscale);
-#pragma unroll
-                    for (int r = 0; r < XP_ROWS; r++)
-#pragma unroll
-                        for (int i = 0; i < 16; i++) acc[r][i] *= unscale;
                 }
+                const int x = tx0 + j;
                 if (!LAST) {
-                    if (mfma_wave) {
+                    float amax = 0.0f;   // F16: max of this wave's stored outputs of the tile
+                    float *const outi = out + img * bt.out_stride;
 #pragma unroll
-                        for (int r = 0; r < XP_ROWS; r++) {
-                            const int y = ty0 + XP_ROWS * g + r, x = tx0 + j;
+                    for (int m = 0; m < MW; m++) {
+                        float bv[16];
+#pragma unroll
+                        for (int i = 0; i < 16; i++) bv[i] = bias[(mt0 + m) * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+#pragma unroll
+                        for (int r = 0; r < XP_WROWS; r++) {
+                            const floatx16 &c = acc[m * XP_WROWS + r];
+                            const int y = ty0 + XP_WROWS * g + r;
                             if (y < Hout && x < Wout) {
 #pragma unroll
                                 for (int q = 0; q < 4; q++) {
-                                    const float4 o = make_float4(fmaxf(acc[r][4 * q] + bv[4 * q], 0.f),
-                                                                 fmaxf(acc[r][4 * q + 1] + bv[4 * q + 1], 0.f),
-                                                                 fmaxf(acc[r][4 * q + 2] + bv[4 * q + 2], 0.f),
-                                                                 fmaxf(acc[r][4 * q + 3] + bv[4 * q + 3], 0.f));
+                                    float o4[4];
+#pragma unroll
+                                    for (int e = 0; e < 4; e++)
+                                        o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bv[4 * q + e])
+                                                           : c[4 * q + e] + bv[4 * q + e]), 0.f);
+                                    const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                                     if (F16) amax = fmaxf(amax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
-                                    const int c = mt * 32 + 8 * q + 4 * h;
-                                    float *dst = OUT_CB ? outi + (((size_t)(c >> 4) * Hout + y) * Wout + x) * 16 + (c & 15)
-                                                        : outi + ((size_t)y * Wout + x) * NF + c;
+                                    const int ch = (mt0 + m) * 32 + 8 * q + 4 * h;
+                                    float *dst = OUT_CB ? outi + (((size_t)(ch >> 4) * Hout + y) * Wout + x) * 16 + (ch & 15)
+                                                        : outi + ((size_t)y * Wout + x) * NF + ch;
                                     if (!(TOWER_DIAG & 16) || o.x == -1.0f) *reinterpret_cast<float4 *>(dst) = o;
                                 }
                             }
                         }
-                        if (F16) {   // outputs are >= +0 (ReLU): their float bits order like their values
+                    }
+                    if (F16) {   // outputs are >= +0 (ReLU): their float bits order like their values
 #pragma unroll
-                            for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-                            if (lane == 0)
-                                atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride),
-                                          __float_as_uint(amax));
-                        }
+                        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+                        if (lane == 0)
+                            atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride),
+                                      __float_as_uint(amax));
                     }
                 } else {
-                    // a pixel's 64 channels live in two waves (mt = 0, 1): the sums of
-                    // squares are exchanged through LDS (every wave joins the barriers)
-                    if (mfma_wave) {
+                    // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm
 #pragma unroll
-                        for (int r = 0; r < XP_ROWS; r++) {
-                            float ss = 0.0f;
+                    for (int r = 0; r < XP_WROWS; r++) {
+                        float v[2][16];
+                        float ss = 0.0f;
+#pragma unroll
+                        for (int m = 0; m < 2; m++)
 #pragma unroll
                             for (int i = 0; i < 16; i++) {
-                                const float vv = acc[r][i] + bv[i];
-                                ss += vv * vv;
+                                const float bb = bias[m * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+                                const float cv = acc[m * XP_WROWS + r][i];
+                                v[m][i] = F16 ? fmaf(cv, unscale, bb) : cv + bb;
+                                ss += v[m][i] * v[m][i];
                             }
-                            ss += __shfl_xor(ss, 32, 64);
-                            if (h == 0) red0[(mt * XP_TY + XP_ROWS * g + r) * XP_TX + j] = ss;
-                        }
-                    }
-                    __syncthreads();
-                    if (mfma_wave) {
+                        ss += __shfl_xor(ss, 32, 64);
+                        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+                        float s2 = 0.0f;
 #pragma unroll
-                        for (int r = 0; r < XP_ROWS; r++) {
-                            const int row = XP_ROWS * g + r;
-                            const float tot = red0[row * XP_TX + j] + red0[(XP_TY + row) * XP_TX + j];
-                            const float inv = 1.0f / sqrtf(fmaxf(tot, 1e-12f));
-                            float v[16];
-                            float s2 = 0.0f;
+                        for (int m = 0; m < 2; m++)
 #pragma unroll
-                            for (int i = 0; i < 16; i++) { v[i] = (acc[r][i] + bv[i]) * inv; s2 += v[i] * v[i]; }
-                            s2 += __shfl_xor(s2, 32, 64);
-                            if (h == 0) red1[(mt * XP_TY + row) * XP_TX + j] = s2;
-                            const int y = ty0 + row, x = tx0 + j;
-                            if (y < Hout && x < Wout) {
-                                const size_t pix = (size_t)y * Wout + x + img * bt.pix_stride;
+                            for (int i = 0; i < 16; i++) { v[m][i] *= inv; s2 += v[m][i] * v[m][i]; }
+                        s2 += __shfl_xor(s2, 32, 64);
+                        const int y = ty0 + XP_WROWS * g + r;
+                        if (y < Hout && x < Wout) {
+                            const size_t pix = (size_t)y * Wout + x + img * bt.pix_stride;   // includes the image
+#pragma unroll
+                            for (int m = 0; m < 2; m++)
 #pragma unroll
                                 for (int q = 0; q < 4; q++) {
-                                    const int c = mt * 32 + 8 * q + 4 * h;
-                                    *reinterpret_cast<float4 *>(out + pix * NF + c) =   // pix includes the image
-                                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                                    const int ch = m * 32 + 8 * q + 4 * h;
+                                    *reinterpret_cast<float4 *>(out + pix * NF + ch) =
+                                        make_float4(v[m][4 * q], v[m][4 * q + 1], v[m][4 * q + 2], v[m][4 * q + 3]);
                                     if (ohi) {
                                         bf16x4 hv, lv;
 #pragma unroll
                                         for (int e = 0; e < 4; e++) {
-                                            const float xv = v[4 * q + e];
+                                            const float xv = v[m][4 * q + e];
                                             const __bf16 hh = (__bf16)xv;
                                             hv[e] = hh;
                                             lv[e] = (__bf16)(xv - (float)hh);
                                         }
-                                        *reinterpret_cast<uint2 *>(ohi + pix * NF + c) = __builtin_bit_cast(uint2, hv);
-                                        *reinterpret_cast<uint2 *>(olo + pix * NF + c) = __builtin_bit_cast(uint2, lv);
+                                        *reinterpret_cast<uint2 *>(ohi + pix * NF + ch) = __builtin_bit_cast(uint2, hv);
+                                        *reinterpret_cast<uint2 *>(olo + pix * NF + ch) = __builtin_bit_cast(uint2, lv);
                                     }
                                 }
-                            }
-                        }
-                    }
-                    __syncthreads();
-                    if (onrm && mfma_wave && mt == 0 && h == 0) {
-#pragma unroll
-                        for (int r = 0; r < XP_ROWS; r++) {
-                            const int row = XP_ROWS * g + r, y = ty0 + row, x = tx0 + j;
-                            if (y < Hout && x < Wout)   // fp32 rounding bound of the 64-term sum
-                                onrm[(size_t)y * Wout + x + img * bt.pix_stride] =
-                                    sqrtf(red1[row * XP_TX + j] + red1[(XP_TY + row) * XP_TX + j]) * 1.000004f;
+                            // fp32 rounding bound of the 64-term sum
+                            if (onrm && h == 0) onrm[pix] = sqrtf(s2) * 1.000004f;
                         }
                     }
                 }

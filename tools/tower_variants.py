@@ -1,14 +1,17 @@
-"""Time one middle tower layer (layer 3, c-block layouts) of each tools/_var/libsde_t<bits>.so
-(see tower_variants.sh) and of the library itself, for bf16x6 and f16x3."""
+"""Time the tower of each tools/_var/libsde_*.so (see tower_variants.sh) and of the library itself:
+one middle layer (layer 3, c-block layouts, one image) in bf16x6 and f16x3, and the whole f16x3
+tower for a pair (sde_tower_forward_batch).  Libraries are timed round-robin, 3 rounds, and the
+median is printed (box clocks drift over a run)."""
 import ctypes
 import glob
 import os
+import statistics
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from scenedepthestimation_amd import mc_cnn, ops  # noqa: E402
+from scenedepthestimation_amd import _lib, mc_cnn, ops  # noqa: E402
 
 H = W = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 L = 5
@@ -17,32 +20,53 @@ hin, win = H + 6, W + 6
 x = torch.rand((hin, win, 64), device="cuda")
 y = torch.empty((hin - 2, win - 2, 64), device="cuda")
 words = torch.ones(2, device="cuda")
+imgs = torch.randn((2, H + 2 * L, W + 2 * L), device="cuda")
+feat = torch.empty((2, H, W, 64), device="cuda")
+nws = ops.tower_batch_workspace_bytes(H, W, 2, L)
+ws = torch.empty(nws, dtype=torch.uint8, device="cuda")
 P, I = ctypes.c_void_p, ctypes.c_int
 here = os.path.dirname(os.path.abspath(__file__))
-sos = sorted(glob.glob(os.path.join(here, "_var", "libsde_*.so")))
-from scenedepthestimation_amd import _lib  # noqa: E402
-for so in [_lib.LIB] + sos:
+sos = [_lib.LIB] + sorted(glob.glob(os.path.join(here, "_var", "libsde_*.so")))
+libs = []
+for so in sos:
     lib = ctypes.CDLL(so)
-    fn = lib.sde_tower_layer_scaled
-    fn.argtypes = [P, I, I, P, I, I, I, P, I, P, P, P, P, P, P]
-    s = torch.cuda.current_stream().cuda_stream
-    for prec, flag in (("bf16x6", 1), ("f16x3", 8)):
-        def run():
-            words[1] = 0
-            rc = fn(x.data_ptr(), hin, win, packed.data_ptr(), L, 64, 3, y.data_ptr(), flag | 2 | 4, None, None, None,
-                    words.data_ptr(), words.data_ptr() + 4, s)
+    lib.sde_tower_layer_scaled.argtypes = [P, I, I, P, I, I, I, P, I, P, P, P, P, P, P]
+    lib.sde_tower_forward_batch.argtypes = [P, I, I, I, P, I, I, P, P, ctypes.c_int64, I, P, P, P, P]
+    libs.append((os.path.basename(so), lib))
+
+
+def timed(fn, n):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+res = {}
+for rnd in range(3):
+    for name, lib in libs:
+        s = torch.cuda.current_stream().cuda_stream
+        for prec, flag in (("bf16x6", 1), ("f16x3", 8)):
+            def run():
+                rc = lib.sde_tower_layer_scaled(x.data_ptr(), hin, win, packed.data_ptr(), L, 64, 3, y.data_ptr(),
+                                                flag | 2 | 4, None, None, None, words.data_ptr(),
+                                                words.data_ptr() + 4, s)
+                assert rc == 0, rc
+            res.setdefault((name, "layer3 " + prec), []).append(timed(run, 20))
+            if "clk" in name and rnd == 0:   # TOWER_DIAG & 128: per-workgroup cycle / 100 MHz-tick deltas
+                st = y.view(-1)[:512].view(256, 2).double()
+                print(f"{name:20s} {prec}: in-kernel clock {(st[:, 0] / st[:, 1] * 0.1).median().item():.3f} GHz, "
+                      f"{st[:, 0].median().item() / 1e3:.0f} kcycles", flush=True)
+
+        def runb():
+            rc = lib.sde_tower_forward_batch(imgs.data_ptr(), 2, H, W, packed.data_ptr(), L, 64, feat.data_ptr(),
+                                             ws.data_ptr(), nws, 8, None, None, None, s)
             assert rc == 0, rc
-        for _ in range(20):
-            run()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(20):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        msg = ""
-        if "clk" in os.path.basename(so):   # TOWER_DIAG & 128: per-workgroup cycle / 100 MHz-tick deltas
-            st = y.view(-1)[:512].view(256, 2).double()
-            ghz = (st[:, 0] / st[:, 1] * 0.1).median().item()
-            msg = f"  in-kernel clock {ghz:.3f} GHz, {st[:, 0].median().item() / 1e3:.0f} kcycles"
-        print(f"{os.path.basename(so):20s} {prec:7s} {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us{msg}", flush=True)
+        res.setdefault((name, "tower pair f16x3"), []).append(timed(runb, 10))
+for (name, what), v in res.items():
+    print(f"{name:20s} {what:18s} {statistics.median(v):8.1f} us   ({' '.join(f'{t:.0f}' for t in v)})", flush=True)
