@@ -126,7 +126,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     def tower_pair(timed):
         """Preprocess both images, then the tower layer by layer with both images per launch
         (sde_tower_layer_batch = what sde_tower_forward_batch launches), layer 3 timed."""
-        e_t = t_tower.start() if timed else None
+        e_t = t_tower.start() if timed == "stages" else None
         for i in range(2):
             ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
         if not batched:   # split planes requested: per-image launches
@@ -152,7 +152,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
             else:   # a contiguous prefix of the ping-pong buffer, viewed at this layer's size
                 o = acts[cur ^ 1][: 2 * (hin - 2) * (win - 2) * NF].view(2, hin - 2, win - 2, NF)
             src = acts[cur][: 2 * hin * win * NF].view(2, hin, win, NF)
-            e = t_conv.start() if (timed and layer == 3) else None
+            e = t_conv.start() if (timed == "conv" and layer == 3) else None
             ops.tower_layer_batch(src, m.packed, L, layer, o, precision=m.tower_precision,
                                   in_cblock=cbl, out_cblock=cbl and layer < L, in_absmax=words[:, layer - 2:layer - 1],
                                   out_absmax=words[:, layer - 1:layer] if layer < L else None)
@@ -165,22 +165,24 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
         m.split_valid = False
 
     if what == "tower+cbca+sgm":
-        def step_sgm(timed=False):
-            e = t_tower.start() if timed else None
+        def step_sgm(timed=None):
+            e = t_tower.start() if timed == "stages" else None
             m.features()
             if e is not None:
                 t_tower.stop(e)
-            e = t_cv.start() if timed else None
+            e = t_cv.start() if timed == "stages" else None
             out = m.sgm_path(post=True)
             if e is not None:
                 t_cv.stop(e)
             return out
         return step_sgm
 
-    def step(timed=False):
+    def step(timed=None):
+        """timed: None (warm-up), "conv" (the timed region: HIP events around the roofline kernel
+        only) or "stages" (after the timed region: events around the tower and the CV+WTA)."""
         if what == "tower+cv_wta":
             tower_pair(timed)
-        e = t_cv.start() if timed else None
+        e = t_cv.start() if timed == "stages" else None
         m.cost_wta()
         if e is not None:
             t_cv.stop(e)
@@ -274,8 +276,8 @@ def main():
         dm = DisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
         dm.m.load_images(left, right)
 
-        def step(timed=False):
-            e = t_tower.start() if timed else None
+        def step(timed=None):
+            e = t_tower.start() if timed == "stages" else None
             r = dm.match()
             if e is not None:
                 t_tower.stop(e)
@@ -299,12 +301,17 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(timed=True)
+        step(timed="conv")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # per-stage times from a few extra steps outside the timed region (their events would add
+    # stream barriers to the timed steps)
+    for _ in range(min(args.steps, 5)):
+        step(timed="stages")
+    torch.cuda.synchronize()
     tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

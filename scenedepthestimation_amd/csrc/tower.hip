@@ -299,7 +299,7 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
 // Profiling builds only (tools/tower_variants.sh): TOWER_DIAG bits switch parts of the
 // persistent kernel off -- 1 stager HBM loads, 2 all stager work, 4 the MFMAs, 8 the MFMA
 // waves' LDS fragment reads, 16 the middle layers' output stores, 32 the per-c-block barriers, 64 the A-fragment reloads
-// (timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
+// (timing only), 256 the epilogue (timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
 // out[2 * blockIdx.x + {0, 1}] (clock check).  0 in the library.
 #ifndef XP_RING_F16
 #define XP_RING_F16 3
@@ -329,7 +329,8 @@ constexpr int XP_ACC = 8;                         // accumulators per MFMA wave
 #define XP_AL(F16, WR) (((WR) == 8 || (F16)) ? 2 : 1)   // A fragments requested this many taps ahead
 constexpr int XP_WX = XP_IX + 2, XP_WIN = (XP_IY + 2) * XP_WX;   // FIRST: image window of a tile (20 x 36)
 // two stages | FIRST: one image window per stager wave
-constexpr size_t XP_SMEM = (size_t)2 * XP_STAGE + 4 * XP_WIN * sizeof(float);
+constexpr size_t XP_BIAS_OFF = (size_t)2 * XP_STAGE + 4 * XP_WIN * sizeof(float);
+constexpr size_t XP_SMEM = XP_BIAS_OFF + NF * sizeof(float);     // + the layer's 64 biases
 constexpr int XP_NCB = NF / 16;                   // c-blocks per pixel
 
 // Split 4 channels and store them into the stage's six planes.
@@ -630,6 +631,27 @@ __device__ __forceinline__ floatx16 mfma_h(bf16x8 a, bf16x8 b, floatx16 c)
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
+// Epilogue stores: buffer descriptors on a per-tile base (wave-uniform), 32-bit per-lane byte
+// offsets with an SGPR row offset; a lane outside the output (x >= Wout) gets XP_OOB, which the
+// descriptor's range check drops -- no exec-mask branches, no 64-bit address math per store.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t XP_NREC = 0x40000000u, XP_OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xp_rsrc(const void *base)
+{
+    const uintptr_t b = (uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)hi << 32) | lo), 0, (int)XP_NREC, 0x00020000);
+}
+
+__device__ __forceinline__ void xp_st4(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
+{
+    if (TOWER_DIAG & 16) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(vo), "s"(so));
+    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
+}
+
 // One c-block for one MFMA wave: 9 taps x 4 output rows = 36 row-steps; each step's B
 // fragment (one input row segment, NP parts) feeds both M-tiles (output channels 0-31 and
 // 32-63): 2 x 6 (bf16x6) or 2 x 3 (F16) MFMAs, small terms first, the leading product last.
@@ -721,8 +743,9 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     constexpr int XP_WROWS = LAST ? 4 : (FIRST ? XP_WR_FIRST : XP_WR_MID), MW = 8 / XP_WROWS;
     static_assert(XP_WROWS == 4 || XP_WROWS == 8, "wave mapping");
     // MFMA wave: output rows XP_WROWS*g .. +XP_WROWS-1, M-tiles mt0 .. mt0+MW-1
-    const int g = XP_WROWS == 4 ? (wave & 3) : ((wave >> 1) & 1);
-    const int mt0 = XP_WROWS == 4 ? 0 : (wave & 1);
+    // wave-uniform by construction; readfirstlane tells the compiler (SGPR row offsets, scalar branches)
+    const int g = __builtin_amdgcn_readfirstlane(XP_WROWS == 4 ? (wave & 3) : ((wave >> 1) & 1));
+    const int mt0 = __builtin_amdgcn_readfirstlane(XP_WROWS == 4 ? 0 : (wave & 1));
     const int st = tid - XP_STAGERS;            // stager thread index (valid when !mfma_wave)
     constexpr int NP = F16 ? 2 : 3;
     constexpr int AL = XP_AL(F16, XP_WROWS);
@@ -755,6 +778,9 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         xp_stager_loop<FIRST, IN_CB, F16>(xsm, in, Hin, Win, bt, st, in_amax, hdr, w1blob, win);
         return;
     }
+    float *lbias = reinterpret_cast<float *>(xsm + XP_BIAS_OFF);
+    if (wave == 0) lbias[lane] = bias[lane];   // published by the first barrier below
+    const float4 *lbias4 = reinterpret_cast<const float4 *>(lbias);
     XpFrag a[MW], an[AL][MW];
 #pragma unroll
     for (int m = 0; m < MW; m++) {
@@ -776,7 +802,10 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         for (int cb = 0; cb < XP_NCB; cb++) {
             const int ncb = (cb + 1) & (XP_NCB - 1);
             xp_cblock<F16, XP_WROWS>(acc, a, an, wf, mt0, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
-            if (cb == XP_NCB - 1) {
+            if ((TOWER_DIAG & 256) && cb == XP_NCB - 1) {   // timing only: no epilogue, accumulators kept live
+#pragma unroll
+                for (int r = 0; r < XP_ACC; r++) asm volatile("" ::"v"(acc[r]));
+            } else if (cb == XP_NCB - 1) {
                 // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
                 // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
                 // opaque copies of the lane coordinates: keep the epilogue's bias loads and
@@ -789,77 +818,124 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                     scales(tile, s_unused, unscale);
                 }
                 const int x = tx0 + j;
+                const bool xok = x < Wout;
+                const int row0 = XP_WROWS * g;   // this wave's first row in the tile
                 if (!LAST) {
-                    float amax = 0.0f;   // F16: max of this wave's stored outputs of the tile
+                    // F16: max of this lane's stored outputs of the tile, as float bits (outputs are >= +0
+                    // after the ReLU, so their bits order like their values: integer max3, no NaN quieting)
+                    uint32_t amax = 0u;
                     float *const outi = out + img * bt.out_stride;
+                    // OUT_CB: [cblk][h][w][16] -> one descriptor per c-block plane, at the tile's first row;
+                    // else [h][w][64]
+                    const uint32_t vo = xok ? (uint32_t)(x * (OUT_CB ? 64 : 256) + 16 * h) : XP_OOB;
+                    const size_t HW = (size_t)Hout * Wout;
 #pragma unroll
                     for (int m = 0; m < MW; m++) {
-                        float bv[16];
+                        float4 b4[4];
 #pragma unroll
-                        for (int i = 0; i < 16; i++) bv[i] = bias[(mt0 + m) * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
+                        for (int q = 0; q < 4; q++) b4[q] = lbias4[((mt0 + m) * 32 + 8 * q + 4 * h) >> 2];
 #pragma unroll
-                        for (int r = 0; r < XP_WROWS; r++) {
-                            const floatx16 &c = acc[m * XP_WROWS + r];
-                            const int y = ty0 + XP_WROWS * g + r;
-                            if (y < Hout && x < Wout) {
+                        for (int qh = 0; qh < 2; qh++) {
+                            const int cblk = 2 * (mt0 + m) + qh;
+                            const __amdgpu_buffer_rsrc_t rs =
+                                xp_rsrc(OUT_CB ? outi + ((size_t)cblk * HW + (size_t)ty0 * Wout) * 16
+                                               : outi + (size_t)ty0 * Wout * NF);
 #pragma unroll
-                                for (int q = 0; q < 4; q++) {
-                                    float o4[4];
+                            for (int r = 0; r < XP_WROWS; r++) {
+                                const floatx16 &c = acc[m * XP_WROWS + r];
+                                if (ty0 + row0 + r < Hout) {   // wave-uniform
+                                    const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
 #pragma unroll
-                                    for (int e = 0; e < 4; e++)
-                                        o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bv[4 * q + e])
-                                                           : c[4 * q + e] + bv[4 * q + e]), 0.f);
-                                    const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
-                                    if (F16) amax = fmaxf(amax, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
-                                    const int ch = (mt0 + m) * 32 + 8 * q + 4 * h;
-                                    float *dst = OUT_CB ? outi + (((size_t)(ch >> 4) * Hout + y) * Wout + x) * 16 + (ch & 15)
-                                                        : outi + ((size_t)y * Wout + x) * NF + ch;
-                                    if (!(TOWER_DIAG & 16) || o.x == -1.0f) *reinterpret_cast<float4 *>(dst) = o;
+                                    for (int ql = 0; ql < 2; ql++) {
+                                        const int q = 2 * qh + ql;
+                                        const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+                                        float o4[4];
+#pragma unroll
+                                        for (int e = 0; e < 4; e++)
+                                            o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]),
+                                                          0.f);
+                                        const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                                        if (F16) {
+                                            amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                                            amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                                        }
+                                        // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
+                                        xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
+                                    }
                                 }
                             }
                         }
                     }
-                    if (F16) {   // outputs are >= +0 (ReLU): their float bits order like their values
+                    if (F16) {
+                        if (!xok) amax = 0u;   // lanes past the output edge stored nothing
 #pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-                        if (lane == 0)
-                            atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride),
-                                      __float_as_uint(amax));
+                        for (int o = 32; o > 0; o >>= 1) amax = max(amax, (uint32_t)__shfl_xor((int)amax, o, 64));
+                        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride), amax);
                     }
                 } else {
-                    // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm
+                    // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm.
+                    // Outputs [h][w][64] (+ bf16 planes, norm bound), descriptors at the tile's first row.
+                    const size_t pix0 = (size_t)img * bt.pix_stride + (size_t)ty0 * Wout;
+                    const __amdgpu_buffer_rsrc_t rs = xp_rsrc(out + pix0 * NF);
+                    const uint32_t vo = xok ? (uint32_t)(x * 256 + 16 * h) : XP_OOB;
 #pragma unroll
                     for (int r = 0; r < XP_WROWS; r++) {
-                        float v[2][16];
+                        // biased value of channel m*32 + 8q + 4h + e (bias re-read from LDS per use: nothing
+                        // but the accumulators stays live across the row)
+                        int hr = h;
+                        asm volatile("" : "+v"(hr));   // per-row opaque copy: no CSE of bias reads across rows
+                        auto val4 = [&](int m, int q, float (&t)[4]) {
+                            const float4 bq4 = lbias4[(m * 32 + 8 * q + 4 * hr) >> 2];
+                            const float bq[4] = {bq4.x, bq4.y, bq4.z, bq4.w};
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const float cv = acc[m * XP_WROWS + r][4 * q + e];
+                                t[e] = F16 ? fmaf(cv, unscale, bq[e]) : cv + bq[e];
+                            }
+                        };
                         float ss = 0.0f;
 #pragma unroll
                         for (int m = 0; m < 2; m++)
 #pragma unroll
-                            for (int i = 0; i < 16; i++) {
-                                const float bb = bias[m * 32 + 8 * (i >> 2) + 4 * h + (i & 3)];
-                                const float cv = acc[m * XP_WROWS + r][i];
-                                v[m][i] = F16 ? fmaf(cv, unscale, bb) : cv + bb;
-                                ss += v[m][i] * v[m][i];
+                            for (int q = 0; q < 4; q++) {
+                                float t[4];
+                                val4(m, q, t);
+#pragma unroll
+                                for (int e = 0; e < 4; e++) ss += t[e] * t[e];
                             }
                         ss += __shfl_xor(ss, 32, 64);
                         const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+                        float v[2][16];
+#pragma unroll
+                        for (int m = 0; m < 2; m++)
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                float t[4];
+                                val4(m, q, t);
+#pragma unroll
+                                for (int e = 0; e < 4; e++) v[m][4 * q + e] = t[e] * inv;
+                            }
                         float s2 = 0.0f;
 #pragma unroll
                         for (int m = 0; m < 2; m++)
 #pragma unroll
-                            for (int i = 0; i < 16; i++) { v[m][i] *= inv; s2 += v[m][i] * v[m][i]; }
+                            for (int i = 0; i < 16; i++) s2 += v[m][i] * v[m][i];
                         s2 += __shfl_xor(s2, 32, 64);
-                        const int y = ty0 + XP_WROWS * g + r;
-                        if (y < Hout && x < Wout) {
-                            const size_t pix = (size_t)y * Wout + x + img * bt.pix_stride;   // includes the image
+                        if (ty0 + row0 + r < Hout) {   // wave-uniform
+                            const uint32_t rowp = (uint32_t)((row0 + r) * Wout);   // pixels from the tile's first row
 #pragma unroll
                             for (int m = 0; m < 2; m++)
 #pragma unroll
-                                for (int q = 0; q < 4; q++) {
-                                    const int ch = m * 32 + 8 * q + 4 * h;
-                                    *reinterpret_cast<float4 *>(out + pix * NF + ch) =
-                                        make_float4(v[m][4 * q], v[m][4 * q + 1], v[m][4 * q + 2], v[m][4 * q + 3]);
-                                    if (ohi) {
+                                for (int q = 0; q < 4; q++)
+                                    xp_st4(make_float4(v[m][4 * q], v[m][4 * q + 1], v[m][4 * q + 2], v[m][4 * q + 3]),
+                                           rs, vo + 4u * (m * 32 + 8 * q), rowp * 256u);
+                            if (ohi) {
+                                const __amdgpu_buffer_rsrc_t rh = xp_rsrc(ohi + pix0 * NF), rl = xp_rsrc(olo + pix0 * NF);
+                                const uint32_t vo2 = xok ? (uint32_t)(x * 128 + 8 * h) : XP_OOB;
+#pragma unroll
+                                for (int m = 0; m < 2; m++)
+#pragma unroll
+                                    for (int q = 0; q < 4; q++) {
                                         bf16x4 hv, lv;
 #pragma unroll
                                         for (int e = 0; e < 4; e++) {
@@ -868,12 +944,17 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                                             hv[e] = hh;
                                             lv[e] = (__bf16)(xv - (float)hh);
                                         }
-                                        *reinterpret_cast<uint2 *>(ohi + pix * NF + ch) = __builtin_bit_cast(uint2, hv);
-                                        *reinterpret_cast<uint2 *>(olo + pix * NF + ch) = __builtin_bit_cast(uint2, lv);
+                                        const uint32_t o2 = vo2 + 2u * (m * 32 + 8 * q);
+                                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rh, o2, rowp * 128u, 0);
+                                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lv), rl, o2, rowp * 128u, 0);
                                     }
-                                }
+                            }
                             // fp32 rounding bound of the 64-term sum
-                            if (onrm && h == 0) onrm[pix] = sqrtf(s2) * 1.000004f;
+                            if (onrm) {
+                                const __amdgpu_buffer_rsrc_t rn = xp_rsrc(onrm + pix0);
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sqrtf(s2) * 1.000004f), rn,
+                                                                      (xok && h == 0) ? (uint32_t)(x * 4) : XP_OOB, rowp * 4u, 0);
+                            }
                         }
                     }
                 }
