@@ -34,6 +34,35 @@ namespace sde {
 // left of the image are zero-filled, so an invalid voxel (x < d) scores exactly
 // +0 = -(-0.0), like the CPU path.
 // ---------------------------------------------------------------------------
+// Arithmetic of the fast scores (unlike the chunked kernels of cost_volume.hip, which use bf16
+// hi/lo): every operand is scaled by 2^RW_S (exact) and split into two fp16 parts, x*2^S = h + l
+// + r; the three partial products run on v_mfma_f32_32x32x16_f16, the eight small-term MFMAs
+// (l*h', h*l') of a tile before the four leading ones (h*h').  Bound per voxel (a = fl[x],
+// b = fr[x-d], Cauchy-Schwarz as in cost_volume.hip):
+//   split: |r| <= 2^-22 |x| 2^S (fp16 11-bit parts) and the dropped l*l' <= 2^-22 |ab| 2^2S
+//          -> 3.001 * 2^-22 * sum|ab|                                         (7.2e-7)
+//   accumulation, the conservative per-add model of cost_volume.hip (2^-23 of the running
+//   sum per product): 128 small-term adds on partial sums <= 2.002 * 2^-11 sum|ab|, then 64
+//   leading adds on partial sums <= 1.002 sum|ab|  -> (64 * 1.002 + 0.13) * 2^-23  (7.7e-6)
+//   NumPy pairwise order of the exact cost: 10 * 2^-24                        (6.0e-7)
+//   -> |s_fast - s_exact| <= RW_K * ||a|| ||b||, RW_K = 1.5e-5 (1.67x margin over 9.0e-6),
+// plus 2^-30 (||a|| + ||b||) for parts that fall into fp16's subnormal range (absolute error
+// 2^-25 per scaled element, 64 elements).  A pixel is certified only when its norm and the
+// window's largest norm are below 2^(15-S) - 1: no part can overflow fp16.
+constexpr int RW_S = 8;
+constexpr float RW_SCALE = 256.0f;                 // 2^RW_S
+constexpr float RW_K = 1.5e-5f;
+constexpr float RW_ABS = 9.3132257e-10f;           // 2^-30
+constexpr float RW_NMAX = 127.0f;                  // norm limit: 127 * 2^8 < 65504
+typedef _Float16 rw_f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void rw_split(float x, _Float16 &h, _Float16 &l)
+{
+    const float xs = x * RW_SCALE;
+    h = (_Float16)xs;
+    l = (_Float16)(xs - (float)h);
+}
+
 constexpr int RW_T = 32;           // pixels per tile (= one MFMA N-tile of left pixels)
 constexpr int RW_WAVES = 8;
 constexpr int RW_NX = RW_T * RW_WAVES;   // left pixels per superstrip (256)
@@ -59,10 +88,10 @@ __device__ __forceinline__ bool rw_nonfinite(float x) { return (__float_as_uint(
 __device__ __forceinline__ void rw_store(uint4 *ring, unsigned *tmax, unsigned *tbad, int slot, int u, float4 v)
 {
     const int px = u >> 4, q = u & 15;
-    __bf16 h0, h1, h2, h3, l0, l1, l2, l3;
-    fx_split(v.x, h0, l0); fx_split(v.y, h1, l1); fx_split(v.z, h2, l2); fx_split(v.w, h3, l3);
-    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
-    const bf4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+    _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
+    rw_split(v.x, h0, l0); rw_split(v.y, h1, l1); rw_split(v.z, h2, l2); rw_split(v.w, h3, l3);
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
     char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
     *reinterpret_cast<uint2 *>(base) = __builtin_bit_cast(uint2, hv);
     *reinterpret_cast<uint2 *>(base + 256 * 16) = __builtin_bit_cast(uint2, lv);
@@ -148,7 +177,7 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
         unsigned nmax2 = 0u, wbad = 0u;     // window: max squared norm (bits), any non-finite tile
         bool lbad = false;
         if (xb < W) {          // wave-uniform: waves past the row end only help with the ring
-            fx_bf16x8 bh[4], bl[4];
+            rw_f16x8 bh[4], bl[4];
             float ssl = 0.0f;
 #pragma unroll
             for (int s = 0; s < 4; s++) {
@@ -156,8 +185,8 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
                 const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
-                    __bf16 hh, ll;
-                    fx_split(v8[e], hh, ll);
+                    _Float16 hh, ll;
+                    rw_split(v8[e], hh, ll);
                     bh[s][e] = hh;
                     bl[s][e] = ll;
                     ssl += v8[e] * v8[e];
@@ -187,15 +216,21 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
                 wbad |= tbad[slot];
                 const uint4 *tp = ring + slot * 512;
                 fx_floatx16 acc = {0};
+                rw_f16x8 ah[4], al[4];
 #pragma unroll
                 for (int s = 0; s < 4; s++) {
                     const int sl = fx_slot(j, 2 * s + h);
-                    const fx_bf16x8 ah = __builtin_bit_cast(fx_bf16x8, tp[sl]);
-                    const fx_bf16x8 al = __builtin_bit_cast(fx_bf16x8, tp[256 + sl]);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[s], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[s], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[s], acc, 0, 0, 0);
+                    ah[s] = __builtin_bit_cast(rw_f16x8, tp[sl]);
+                    al[s] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
                 }
+                // the small terms first, then the leading products (the order the bound assumes)
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s], bh[s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bl[s], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int s = 0; s < 4; s++) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s], bh[s], acc, 0, 0, 0);
                 const int dl = dt + j - 4 * h;             // d of register r is dl - ((r&3) + 8(r>>2))
                 if (dlo >= d0 && dhi < d1) {
 #pragma unroll
@@ -242,10 +277,13 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
         }
         // certificate and outputs (off the ring: overlaps the stores)
         if (xb < W && h == 0 && xok) {
-            const float eps = FX_K * nl * (sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP) + FX_ABS;
+            // scores are scaled by 2^2S (exact): compare against the scaled bound
+            const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
+            const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
             const size_t p = rowpix + x;
-            // certified only when every operand is finite (then every score and eps are finite too)
-            if (!lbad && !wbad && (best - second) > 2.0f * eps && arg >= 0) {
+            // certified only when every operand is finite and no fp16 part can overflow (then
+            // every score and eps are finite too)
+            if (!lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX && (best - second) > 2.0f * eps && arg >= 0) {
                 if (WANT_MIN) {
                     float cost = -0.0f;
                     if (x - arg >= 0)
