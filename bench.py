@@ -127,8 +127,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
         """Preprocess both images, then the tower layer by layer with both images per launch
         (sde_tower_layer_batch = what sde_tower_forward_batch launches), layer 3 timed."""
         e_t = t_tower.start() if timed == "stages" else None
-        for i in range(2):
-            ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
+        ops.preprocess_u8_batch(m.img_u82, L, out=m.img_pad2, stats=m.stats2)
         if not batched:   # split planes requested: per-image launches
             m.features_from_padded()
             if e_t is not None:
@@ -138,8 +137,7 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
         cbl = m.tower_precision in ("bf16x6", "f16x3")
         if m.tower_precision == "f16x3":
             words.zero_()
-            for i in range(2):
-                ops.absmax(m.img_pad[i], words[i, 0:1])
+            ops.absmax_batch(m.img_pad2, words)
         hin, win = H + 2 * L - 4, W + 2 * L - 4
         first_out = acts[0][: 2 * hin * win * NF].view(2, hin, win, NF) if L > 2 else m.feat2
         ops.tower_layer_batch(m.img_pad2, m.packed, L, 2, first_out, precision=m.tower_precision,

@@ -217,6 +217,9 @@ int sde_tower_layer_batch(const float *in, int nimg, int64_t in_stride, int Hin,
                           int nlayers, int nf, int layer, float *out, int64_t out_stride, int flags,
                           const float *in_absmax, float *out_absmax, int amax_stride, void *stream);
 
+/* sde_absmax_f32 over nimg arrays of n floats (x + i * n) into absmax[i * absmax_stride]. */
+int sde_absmax_f32_batch(const float *x, int nimg, int64_t n, float *absmax, int absmax_stride, void *stream);
+
 /* *absmax = max(*absmax, max |x[i]|) over n floats (float bits compared as integers; *absmax >= +0). */
 int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream);
 
@@ -230,6 +233,11 @@ int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream);
 #define SDE_PREPROCESS_SCRATCH_BYTES 16
 int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,
                       void *stream);
+
+/* sde_preprocess_u8 over nimg images in one pair of launches: imgs [nimg][H][W],
+ * out_pad [nimg][H+2*pad][W+2*pad], scratch nimg * SDE_PREPROCESS_SCRATCH_BYTES. */
+int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int W, int pad, float *out_pad, void *scratch,
+                            void *stream);
 
 /* ---------------------------------------------------------------------- */
 /* Semi-global matching (GPU path of disparity_compute_by_gpu,               */

@@ -972,8 +972,11 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
 // max |x| over n floats, atomically maxed (as float bits) into *amax (F16 tower scaling):
 // float4 grid-stride loads, one atomic per workgroup.
-__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ x, int64_t n, float *__restrict__ amax)
+__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ x, int64_t n, float *__restrict__ amax,
+                                                     int amax_stride)
 {
+    x += blockIdx.y * n;        // batch: image blockIdx.y -> amax[blockIdx.y * amax_stride]
+    amax += blockIdx.y * amax_stride;
     float m = 0.0f;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
     const int64_t head = std::min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(x) & 15)) / 4 & 3);
@@ -1023,6 +1026,8 @@ __global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict
 __global__ __launch_bounds__(256) void image_sums_kernel(const uint8_t *__restrict__ img, int64_t n,
                                                          unsigned long long *__restrict__ sums)
 {
+    img += blockIdx.y * n;      // batch: image blockIdx.y, its two sums at sums[2 * blockIdx.y]
+    sums += 2 * blockIdx.y;
     unsigned long long s = 0, q = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
     for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
@@ -1065,6 +1070,9 @@ __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restric
                                                         float *__restrict__ out)
 {
     const int Wp = W + 2 * pad;
+    img += (size_t)blockIdx.y * H * W;      // batch: image blockIdx.y
+    sums += 2 * blockIdx.y;
+    out += (size_t)blockIdx.y * (H + 2 * pad) * Wp;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)(H + 2 * pad) * Wp) return;
     const double n = (double)H * W;
@@ -1351,7 +1359,17 @@ SDE_EXPORT int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *st
     if (n == 0) return SDE_OK;
     if (!x) return SDE_ERR_ARG;
     const int blocks = (int)std::min<int64_t>(256, cdiv(n, 256 * 16));
-    absmax_kernel<<<blocks, 256, 0, as_stream(stream)>>>(x, n, absmax);
+    absmax_kernel<<<blocks, 256, 0, as_stream(stream)>>>(x, n, absmax, 0);
+    return launch_status();
+}
+
+SDE_EXPORT int sde_absmax_f32_batch(const float *x, int nimg, int64_t n, float *absmax, int absmax_stride, void *stream)
+{
+    if (!absmax || n < 0 || nimg <= 0 || nimg > 65535 || absmax_stride < 0) return SDE_ERR_ARG;
+    if (n == 0) return SDE_OK;
+    if (!x) return SDE_ERR_ARG;
+    const int blocks = (int)std::min<int64_t>(std::max(1, 256 / nimg), cdiv(n, 256 * 16));
+    absmax_kernel<<<dim3(blocks, nimg), 256, 0, as_stream(stream)>>>(x, n, absmax, absmax_stride);
     return launch_status();
 }
 
@@ -1389,10 +1407,9 @@ SDE_EXPORT int sde_tower_forward_batch(const float *img_pad, int nimg, int H, in
     if (f16) {
         if (nlayers > AS) return SDE_ERR_ARG;
         if (hipMemsetAsync(amax, 0, nimg * TOWER_AMAX_BYTES, st) != hipSuccess) return SDE_ERR_LAUNCH;
-        for (int i = 0; i < nimg; i++) {
-            const int rc = sde_absmax_f32(img_pad + i * img_stride, img_stride, amax + i * AS, stream);
-            if (rc != SDE_OK) return rc;
-        }
+        // one launch for the batch: per-image bound words amax[i * AS]
+        const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, 256 / nimg), cdiv(img_stride, 256 * 16));
+        absmax_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(img_pad, img_stride, amax, AS);
     }
     int hin = Hp, win = Wp;
     // intermediate activations in the c-block-major layout on the split paths
@@ -1421,17 +1438,24 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
                                    feat_hi, feat_lo, feat_norm, stream);
 }
 
+SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int W, int pad, float *out_pad,
+                                       void *scratch, void *stream)
+{
+    if (!imgs || !out_pad || !scratch || nimg <= 0 || nimg > 65535 || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
+    hipStream_t st = as_stream(stream);
+    unsigned long long *sums = reinterpret_cast<unsigned long long *>(scratch);
+    if (hipMemsetAsync(sums, 0, (size_t)nimg * 2 * sizeof(unsigned long long), st) != hipSuccess)
+        return SDE_ERR_LAUNCH;
+    const int64_t npix = (int64_t)H * W;
+    const int blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(npix, 256 * 4 * 8)));
+    image_sums_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(imgs, npix, sums);
+    const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
+    znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256), nimg), 256, 0, st>>>(imgs, H, W, pad, sums, out_pad);
+    return launch_status();
+}
+
 SDE_EXPORT int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,
                                  void *stream)
 {
-    if (!img || !out_pad || !scratch || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
-    hipStream_t st = as_stream(stream);
-    unsigned long long *sums = reinterpret_cast<unsigned long long *>(scratch);
-    if (hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return SDE_ERR_LAUNCH;
-    const int64_t npix = (int64_t)H * W;
-    const int blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(npix, 256 * 4 * 8)));
-    image_sums_kernel<<<blocks, 256, 0, st>>>(img, npix, sums);
-    const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
-    znorm_pad_kernel<<<cdiv(n, 256), 256, 0, st>>>(img, H, W, pad, sums, out_pad);
-    return launch_status();
+    return sde_preprocess_u8_batch(img, 1, H, W, pad, out_pad, scratch, stream);
 }

@@ -305,6 +305,18 @@ def tower_forward_batch(img_pad, packed, nlayers: int, nf: int = 64, out=None, w
     return out
 
 
+def absmax_batch(x, out):
+    """out [N, k] (f32 device, column 0 used) = max(out, max |x[i]|) per image i of x [N, ...]
+    (sde_absmax_f32_batch, one launch)."""
+    N = x.shape[0]
+    _need(x, "absmax input")
+    if out.dtype != torch.float32 or not out.is_cuda or out.shape[0] != N or out.stride(1) != 1:
+        raise ValueError("absmax words must be a float32 [N, k] device tensor with unit column stride")
+    check(lib.sde_absmax_f32_batch(x.data_ptr(), N, x[0].numel(), out.data_ptr(), out.stride(0), _stream()),
+          "sde_absmax_f32_batch")
+    return out
+
+
 def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
                 in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
     """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
@@ -376,6 +388,21 @@ def preprocess_u8(img_u8, pad: int, out=None, stats=None):
     check(lib.sde_preprocess_u8(pi, H, W, pad, _need(out, "out_pad", shape=(H + 2 * pad, W + 2 * pad)),
                                 _need(stats, "scratch", dtype=torch.uint8, shape=(PREPROCESS_SCRATCH_BYTES,)),
                                 _stream()), "sde_preprocess_u8")
+    return out
+
+
+def preprocess_u8_batch(imgs_u8, pad: int, out=None, stats=None):
+    """u8 [N,H,W] -> zero-padded z-normalised f32 [N, H+2p, W+2p], all images per launch.
+    stats: optional uint8 scratch tensor of N * PREPROCESS_SCRATCH_BYTES bytes."""
+    N, H, W = imgs_u8.shape
+    pi = _need(imgs_u8, "images", dtype=torch.uint8)
+    if out is None:
+        out = _empty((N, H + 2 * pad, W + 2 * pad), torch.float32, imgs_u8)
+    if stats is None:
+        stats = _empty((N * PREPROCESS_SCRATCH_BYTES,), torch.uint8, imgs_u8)
+    check(lib.sde_preprocess_u8_batch(pi, N, H, W, pad, _need(out, "out_pad", shape=(N, H + 2 * pad, W + 2 * pad)),
+                                      _need(stats, "scratch", dtype=torch.uint8, shape=(N * PREPROCESS_SCRATCH_BYTES,)),
+                                      _stream()), "sde_preprocess_u8_batch")
     return out
 
 

@@ -42,11 +42,14 @@ class StereoMatcher:
         dev = self.device
         H, W, L = self.H, self.W, self.nlayers
         self.packed = torch.from_numpy(packed).to(dev)
-        self.img_u8 = [torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.img_u82 = torch.empty((2, H, W), dtype=torch.uint8, device=dev)
+        self.img_u8 = [self.img_u82[0], self.img_u82[1]]
         # both images in one allocation: the tower runs the pair per launch (sde_tower_forward_batch)
         self.img_pad2 = torch.empty((2, H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev)
         self.img_pad = [self.img_pad2[0], self.img_pad2[1]]
-        self.stats = [torch.empty((ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.stats2 = torch.empty((2 * ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=dev)
+        n = ops.PREPROCESS_SCRATCH_BYTES
+        self.stats = [self.stats2[:n], self.stats2[n:]]
         self.feat2 = torch.empty((2, H, W, nf), dtype=torch.float32, device=dev)
         self.feat = [self.feat2[0], self.feat2[1]]
         nws = ops.tower_batch_workspace_bytes(H, W, 2, L, nf)
@@ -75,8 +78,7 @@ class StereoMatcher:
 
     def features(self):
         """Preprocess + tower for both images (compute_feature, process_functional.py:11-45)."""
-        for i in range(2):
-            ops.preprocess_u8(self.img_u8[i], self.nlayers, out=self.img_pad[i], stats=self.stats[i])
+        ops.preprocess_u8_batch(self.img_u82, self.nlayers, out=self.img_pad2, stats=self.stats2)
         return self.features_from_padded()
 
     def features_from_padded(self):

@@ -672,3 +672,22 @@ def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
                                   out_absmax=words[:, layer - 1:layer] if layer < L else None)
             x = y
         assert torch.equal(x, out)
+
+
+def test_preprocess_and_absmax_batch(gpu):
+    """sde_preprocess_u8_batch / sde_absmax_f32_batch (one launch per batch) == the per-image calls."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(3)
+    N, H, W, P = 3, 37, 61, 5
+    imgs = torch.from_numpy(rng.integers(0, 256, (N, H, W), dtype=np.uint8)).cuda()
+    imgs[1] = imgs[1] // 7          # a different range per image
+    out = ops.preprocess_u8_batch(imgs, P)
+    words = torch.zeros((N, 4), device="cuda")
+    ops.absmax_batch(out, words)
+    for i in range(N):
+        single = ops.preprocess_u8(imgs[i].contiguous(), P)
+        assert torch.equal(out[i], single)
+        w = torch.zeros(1, device="cuda")
+        ops.absmax(single, w)
+        assert float(words[i, 0]) == float(w[0]) == float(single.abs().max())
+        assert torch.all(words[i, 1:] == 0)
