@@ -69,7 +69,11 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     constexpr int PF = 16;             // prefetch distance (vmcnt saturates at 63 outstanding ops)
     static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && RS % PF == 0, "ring sizes");
     __shared__ double sP[RS * 64];
-    __shared__ int sN[VERT ? RS * 64 : 1];
+    // support-count prefixes mod 2^16: a support holds at most (2R+1)^2 < 2^16 pixels, so the
+    // difference of two ring entries taken mod 2^16 is the exact count (half the LDS of int32:
+    // more line-waves per CU)
+    static_assert((2 * R + 1) * (2 * R + 1) < 65536, "support counts must fit 16 bits");
+    __shared__ uint16_t sN[VERT ? RS * 64 : 1];
     const int lane = threadIdx.x;
     // Lanes past D work on d = D-1: they compute lane D-1's value and store it to the
     // same address, so no load, LDS access or store in the scan is predicated.
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     }
 
     double P_acc = 0.0;
-    int N_acc = 0;
+    uint32_t N_acc = 0;
     float cr[PF];
     uint32_t ar[PF], br[PF];
     uint32_t sup[U];    // VERT: (up | down << 8) of the last U positions; else (left | right << 8)
@@ -128,8 +132,8 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
         P_acc += (double)cr[slot];
         sP[j * 64 + lane] = P_acc;
         if (VERT) {
-            N_acc += l + r + 1;
-            sN[j * 64 + lane] = N_acc;
+            N_acc += (uint32_t)(l + r + 1);
+            sN[j * 64 + lane] = (uint16_t)N_acc;
             sup[j % U] = min((a >> 16) & 255, (b >> 16) & 255) | (min(a >> 24, b >> 24) << 8);
         } else {
             sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
             const int ib = ((j - R + hi) & (RS - 1)) * 64 + lane, ia = ((j - R - lo - 1) & (RS - 1)) * 64 + lane;
             const double pb = sP[ib], pa = sP[ia];
             float out;
-            if (VERT) out = (float)((pb - pa) / (double)(sN[ib] - sN[ia]));
+            if (VERT) out = (float)((pb - pa) / (double)(uint16_t)(sN[ib] - sN[ia]));
             else out = (float)(pb - pa);
             const int so = VERT ? (int)((uint32_t)(y - qb) * linebytes) : 4 * y * D;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, d4, so, 0);
