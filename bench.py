@@ -422,6 +422,16 @@ def main():
                 ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=m.feat[0], workspace=m.ws,
                                   precision=m.tower_precision)
                 stages[f"tower_{m.tower_precision}_vs_fp32_max_abs"] = float((ref - m.feat[0]).abs().max().item())
+            # the reference's boundary hands over host arrays: host u8 pair in -> host float disparity
+            # out, PCIe copies and synchronisation included (reported beside `value`, never as it)
+            for _ in range(2):
+                m.load_images(left, right)
+                m.match().cpu()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                m.load_images(left, right)
+                m.match().cpu()
+            stages["ms_per_pair_host_io"] = (time.perf_counter() - t0) / 5 * 1e3
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             kname = ("cv_wta_row_kernel + cv_wta_fixup_kernel (certified fused cost volume + WTA)"
