@@ -449,22 +449,7 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
     xp_tile(bt, t, img, ty0, tx0);
     in += img * bt.in_stride;
     if (FIRST) {
-        if (cb == 0) {
-            // a new tile: this wave's copy of the tile's image window (wave-private: no barrier;
-            // a wave's LDS accesses complete in order)
-            const int lane = st & 63;
-#pragma unroll
-            for (int k = 0; k < (XP_WIN + 63) / 64; k++) {
-                const int idx = lane + 64 * k;
-                if (idx < XP_WIN) {
-                    const int iy = idx / XP_WX, ix = idx - iy * XP_WX;
-                    const int y = ty0 + iy, x = tx0 + ix;
-                    win[idx] = (y < Hin && x < Win) ? in[(size_t)y * Win + x] : 0.0f;
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the window's LDS writes have landed
-            __builtin_amdgcn_wave_barrier();
-        }
+        // the tile's image window is already in the wave's LDS window (xp_stager_loop)
         // the thread's chunk is st & 3 for every unit (XP_STAGERS is a multiple of 4)
         const int n0 = cb * 16 + (st & 3) * 4;
         const float4 b = *reinterpret_cast<const float4 *>(w1blob + n0);
@@ -528,14 +513,41 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
         // conv1 on the stagers: each step computed from the wave's LDS image window, one stage ahead
         int sc_img = -1;
         float s = 1.0f, unscale = 1.0f;
+        // the image window of a tile, loaded into registers 3 steps before its first use (while
+        // the previous tile's c-blocks are computed) and written to the wave's LDS window when
+        // the tile's first c-block is filled -- the HBM latency stays off the stagers' path
+        constexpr int WPL = (XP_WIN + 63) / 64;
+        float wv[WPL];
+        const int lane = st & 63;
+        auto wload = [&](int t) {
+            int img, ty0, tx0;
+            xp_tile(bt, t, img, ty0, tx0);
+            const float *src = in + img * bt.in_stride;
+#pragma unroll
+            for (int k = 0; k < WPL; k++) {
+                const int idx = lane + 64 * k;
+                const int iy = idx / XP_WX, ix = idx - iy * XP_WX;
+                const int y = ty0 + iy, x = tx0 + ix;
+                wv[k] = (idx < XP_WIN && y < Hin && x < Win) ? src[(size_t)y * Win + x] : 0.0f;
+            }
+        };
         auto fill = [&](int i) {
-            const int t = tile0 + (i / XP_NCB) * gstride, im = t / bt.tiles_img;
+            const int t = tile0 + (i / XP_NCB) * gstride, im = t / bt.tiles_img, cb = i % XP_NCB;
             if (F16 && im != sc_img) {
                 xp_scales(true, in_amax + im * bt.amax_stride, hdr, s, unscale);
                 sc_img = im;
             }
-            xp_fill<true, false, F16>(xsm + (i & 1) * XP_STAGE, in, Hin, Win, w1blob, t, bt, i % XP_NCB, st, s, win);
+            if (cb == 0) {   // a wave's LDS accesses complete in order: no barrier needed
+#pragma unroll
+                for (int k = 0; k < WPL; k++)
+                    if (lane + 64 * k < XP_WIN) win[lane + 64 * k] = wv[k];
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the window's LDS writes have landed
+                __builtin_amdgcn_wave_barrier();
+            }
+            xp_fill<true, false, F16>(xsm + (i & 1) * XP_STAGE, in, Hin, Win, w1blob, t, bt, cb, st, s, win);
+            if (cb == 1 && t + gstride < bt.ntiles) wload(t + gstride);
         };
+        wload(tile0);
         fill(0);
         __syncthreads();
 #pragma unroll 1
