@@ -299,7 +299,7 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
 // Profiling builds only (tools/tower_variants.sh): TOWER_DIAG bits switch parts of the
 // persistent kernel off -- 1 stager HBM loads, 2 all stager work, 4 the MFMAs, 8 the MFMA
 // waves' LDS fragment reads, 16 the middle layers' output stores, 32 the per-c-block barriers, 64 the A-fragment reloads
-// (timing only), 256 the epilogue (timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
+// (timing only), 256 the epilogue (timing only), 512 the staged values (loads kept; timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
 // out[2 * blockIdx.x + {0, 1}] (clock check).  0 in the library.
 #ifndef XP_RING_F16
 #define XP_RING_F16 3
@@ -582,6 +582,12 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
 #pragma unroll
         for (int k = 0; k < XP_UPT; k++) {
             const int u = st + k * XP_STAGERS;
+            if (TOWER_DIAG & 512) {   // timing only: the loads are made, their values replaced
+                float4 c = v[k];
+                asm volatile("" : "+v"(c.x), "+v"(c.y), "+v"(c.z), "+v"(c.w));
+                if (u < XP_UNITS) xp_store<F16>(sb, u, make_float4(u * 1e-3f, 0.5f, 0.25f, c.x * 0.f), s);
+                continue;
+            }
             if (u < XP_UNITS) xp_store<F16>(sb, u, v[k], s);
         }
     };

@@ -1,7 +1,7 @@
 # Profiling builds of the persistent tower kernel -> tools/_var/libsde_t<name>.so, each built with
 # the -D options given as NAME=OPTS arguments (e.g. t2="-DTOWER_DIAG=2" r4="-DXP_RING_F16=4").
 # TOWER_DIAG bits: 1 stager HBM loads, 2 all stager work, 4 MFMAs, 8 MFMA-wave LDS reads,
-# 16 middle-layer output stores.  Run here (CPU), then time on the GPU with tools/tower_variants.py.
+# 16 middle-layer output stores, 512 staged values replaced by constants (loads kept).  Run here (CPU), then time on the GPU with tools/tower_variants.py.
 set -e
 cd "$(dirname "$0")/.."
 rm -rf tools/_var; mkdir -p tools/_var
