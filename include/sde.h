@@ -315,6 +315,16 @@ int sde_cbca_arms(const float *img, int64_t pitch, int H, int W, int L1, float t
 int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W, int D,
              int side, int L1, int iters, void *stream);
 
+/*
+ * sde_cbca on both volumes of a pair in one launch per pass (same results as
+ * sde_cbca(cv_l, tmp_l, arms_l, arms_r, SDE_SIDE_LEFT) and sde_cbca(cv_r,
+ * tmp_r, arms_r, arms_l, SDE_SIDE_RIGHT)); the four buffers must be distinct.
+ * Build-defined like sde_cbca: the reference only names the aggregated
+ * volumes d_cost_volumel/r_after_aggr (process_functional.py:268,347).
+ */
+int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_r, const uint32_t *arms_l,
+                  const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *stream);
+
 /* is_error_match_kernel (process_functional.py:977-1000): lrc_l/lrc_r u8 [H][W], caller-zeroed. */
 int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,
                  void *stream);

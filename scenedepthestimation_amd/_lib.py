@@ -72,6 +72,7 @@ SIGNATURES = {
     "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_cbca_arms": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]),
     "sde_cbca": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p]),
+    "sde_cbca_pair": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
     "sde_lr_check": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_lrc_fill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sde_median5": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),

@@ -59,21 +59,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cb_rsrc(const void *base, uint
     return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// One launch covers up to two volumes (grid.z): the left- and right-referenced volumes of a pair
+// are independent, and one launch of both fills the machine in whole rounds of line-waves (a
+// 1024^2 x 192 pass has 3072 line-waves per volume against 2048-2560 resident: alone, its second
+// round runs half empty).
+struct CbcaVolumes {
+    const float *src[2];
+    float *dst[2];
+    const uint32_t *ref[2], *oth[2];
+    int side[2];
+};
+
+// The scan of one line of one volume (SIDE compile-time: each launch holds both instantiations
+// and picks one per workgroup).
 template <int R, bool VERT, int SIDE>
-__global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__ src, float *__restrict__ dst,
-                                                       const uint32_t *__restrict__ ref,
-                                                       const uint32_t *__restrict__ oth, int H, int W, int D)
+__device__ __forceinline__ void cbca_scan(const float *__restrict__ src, float *__restrict__ dst,
+                                          const uint32_t *__restrict__ ref, const uint32_t *__restrict__ oth,
+                                          int H, int W, int D, double *__restrict__ sP, uint16_t *__restrict__ sN)
 {
     constexpr int RS = 2 * R + 2;      // prefix ring: positions [f - 2R - 1, f]; also the unroll
     constexpr int U = R + 1;           // support ring (trailing output reads the slot of f - R)
     constexpr int PF = 16;             // prefetch distance (vmcnt saturates at 63 outstanding ops)
     static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && RS % PF == 0, "ring sizes");
-    __shared__ double sP[RS * 64];
-    // support-count prefixes mod 2^16: a support holds at most (2R+1)^2 < 2^16 pixels, so the
-    // difference of two ring entries taken mod 2^16 is the exact count (half the LDS of int32:
-    // more line-waves per CU)
-    static_assert((2 * R + 1) * (2 * R + 1) < 65536, "support counts must fit 16 bits");
-    __shared__ uint16_t sN[VERT ? RS * 64 : 1];
     const int lane = threadIdx.x;
     // Lanes past D work on d = D-1: they compute lane D-1's value and store it to the
     // same address, so no load, LDS access or store in the scan is predicated.
@@ -118,7 +125,12 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
         } else {
             cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, d4, 4 * q * D, 0));
             ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q, 0);
-            const uint32_t o4 = SIDE == SDE_SIDE_LEFT ? 4u * (uint32_t)q - d4 : 4u * (uint32_t)q + d4;
+            uint32_t o4 = SIDE == SDE_SIDE_LEFT ? 4u * (uint32_t)q - d4 : 4u * (uint32_t)q + d4;
+            // opaque: the whole offset must reach the range check as voffset.  Left to itself the
+            // compiler moves the step's constant part of q into the instruction offset, and a
+            // voffset that wrapped below zero (x - d < 0 at the block start, >= 0 at this step)
+            // then fails the check and reads 0 for a pixel inside the row.
+            asm volatile("" : "+v"(o4));
             br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, o4, 0, 0);
         }
     };
@@ -189,15 +201,50 @@ __global__ __launch_bounds__(64) void cbca_scan_kernel(const float *__restrict__
     }
 }
 
-template <int R, int SIDE>
-static void cbca_iters(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D,
-                       int iters, hipStream_t st)
+template <int R, bool VERT>
+__global__ __launch_bounds__(64) void cbca_scan_kernel(const CbcaVolumes vols, int H, int W, int D)
+{
+    constexpr int RS = 2 * R + 2;
+    __shared__ double sP[RS * 64];
+    // support-count prefixes mod 2^16: a support holds at most (2R+1)^2 < 2^16 pixels, so the
+    // difference of two ring entries taken mod 2^16 is the exact count (half the LDS of int32:
+    // more line-waves per CU)
+    static_assert((2 * R + 1) * (2 * R + 1) < 65536, "support counts must fit 16 bits");
+    __shared__ uint16_t sN[VERT ? RS * 64 : 1];
+    const int z = blockIdx.z;
+    if (vols.side[z] == SDE_SIDE_LEFT)
+        cbca_scan<R, VERT, SDE_SIDE_LEFT>(vols.src[z], vols.dst[z], vols.ref[z], vols.oth[z], H, W, D, sP, sN);
+    else
+        cbca_scan<R, VERT, SDE_SIDE_RIGHT>(vols.src[z], vols.dst[z], vols.ref[z], vols.oth[z], H, W, D, sP, sN);
+}
+
+template <int R>
+static void cbca_iters(const CbcaVolumes &fwd, const CbcaVolumes &bwd, int nvol, int H, int W, int D, int iters,
+                       hipStream_t st)
 {
     const int ndc = (D + 63) / 64;
     for (int it = 0; it < iters; it++) {
-        cbca_scan_kernel<R, false, SIDE><<<dim3(ndc, H), 64, 0, st>>>(cv, tmp, ref, oth, H, W, D);
-        cbca_scan_kernel<R, true, SIDE><<<dim3(ndc, W), 64, 0, st>>>(tmp, cv, ref, oth, H, W, D);
+        cbca_scan_kernel<R, false><<<dim3(ndc, H, nvol), 64, 0, st>>>(fwd, H, W, D);
+        cbca_scan_kernel<R, true><<<dim3(ndc, W, nvol), 64, 0, st>>>(bwd, H, W, D);
     }
+}
+
+// fwd: horizontal pass cv -> tmp; bwd: vertical pass tmp -> cv
+static int cbca_launch(float *const cv[2], float *const tmp[2], const uint32_t *const ref[2],
+                       const uint32_t *const oth[2], const int side[2], int nvol, int H, int W, int D, int L1,
+                       int iters, hipStream_t st)
+{
+    CbcaVolumes fwd{}, bwd{};
+    for (int k = 0; k < nvol; k++) {
+        fwd.src[k] = cv[k], fwd.dst[k] = tmp[k];
+        bwd.src[k] = tmp[k], bwd.dst[k] = cv[k];
+        fwd.ref[k] = bwd.ref[k] = ref[k];
+        fwd.oth[k] = bwd.oth[k] = oth[k];
+        fwd.side[k] = bwd.side[k] = side[k];
+    }
+    if (L1 <= 16) cbca_iters<15>(fwd, bwd, nvol, H, W, D, iters, st);
+    else cbca_iters<31>(fwd, bwd, nvol, H, W, D, iters, st);
+    return launch_status();
 }
 
 }  // namespace sde
@@ -219,13 +266,26 @@ SDE_EXPORT int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const u
         L1 > SDE_CBCA_MAX_L1 || (side != SDE_SIDE_LEFT && side != SDE_SIDE_RIGHT) || cv == tmp)
         return SDE_ERR_ARG;
     if (H > 65535 || W > 65535) return SDE_ERR_ARG;      // grid.y = lines
-    hipStream_t st = as_stream(stream);
-    if (side == SDE_SIDE_LEFT) {
-        if (L1 <= 16) cbca_iters<15, SDE_SIDE_LEFT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
-        else cbca_iters<31, SDE_SIDE_LEFT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
-    } else {
-        if (L1 <= 16) cbca_iters<15, SDE_SIDE_RIGHT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
-        else cbca_iters<31, SDE_SIDE_RIGHT>(cv, tmp, arms_ref, arms_other, H, W, D, iters, st);
-    }
-    return launch_status();
+    float *const cvs[2] = {cv, nullptr}, *const tmps[2] = {tmp, nullptr};
+    const uint32_t *const refs[2] = {arms_ref, nullptr}, *const oths[2] = {arms_other, nullptr};
+    const int sides[2] = {side, side};
+    return cbca_launch(cvs, tmps, refs, oths, sides, 1, H, W, D, L1, iters, as_stream(stream));
+}
+
+SDE_EXPORT int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_r, const uint32_t *arms_l,
+                             const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *stream)
+{
+    if (!cv_l || !tmp_l || !cv_r || !tmp_r || !arms_l || !arms_r || H <= 0 || W <= 0 || D <= 0 || iters < 0 ||
+        L1 < 1 || L1 > SDE_CBCA_MAX_L1)
+        return SDE_ERR_ARG;
+    // four distinct buffers: each volume's passes run concurrently with the other's
+    const float *b[4] = {cv_l, tmp_l, cv_r, tmp_r};
+    for (int i = 0; i < 4; i++)
+        for (int j = i + 1; j < 4; j++)
+            if (b[i] == b[j]) return SDE_ERR_ARG;
+    if (H > 65535 || W > 65535) return SDE_ERR_ARG;
+    float *const cvs[2] = {cv_l, cv_r}, *const tmps[2] = {tmp_l, tmp_r};
+    const uint32_t *const refs[2] = {arms_l, arms_r}, *const oths[2] = {arms_r, arms_l};
+    const int sides[2] = {SDE_SIDE_LEFT, SDE_SIDE_RIGHT};
+    return cbca_launch(cvs, tmps, refs, oths, sides, 2, H, W, D, L1, iters, as_stream(stream));
 }

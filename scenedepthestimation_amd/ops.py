@@ -512,6 +512,20 @@ def cbca(cv_hwd, arms_ref, arms_other, side="left", L1=14, iters=2, tmp=None):
     return cv_hwd
 
 
+def cbca_pair(cv_l, cv_r, arms_l, arms_r, L1=14, iters=2, tmp_l=None, tmp_r=None):
+    """cbca(cv_l, arms_l, arms_r, "left") and cbca(cv_r, arms_r, arms_l, "right") in one launch per pass
+    (sde_cbca_pair), in place; tmp_l / tmp_r: same-size scratch, distinct from every volume."""
+    H, W, D = cv_l.shape
+    tmp_l = torch.empty_like(cv_l) if tmp_l is None else tmp_l
+    tmp_r = torch.empty_like(cv_l) if tmp_r is None else tmp_r
+    check(lib.sde_cbca_pair(_need(cv_l, "cost volume"), _need(tmp_l, "tmp", shape=(H, W, D)),
+                            _need(cv_r, "cost volume", shape=(H, W, D)), _need(tmp_r, "tmp", shape=(H, W, D)),
+                            _need(arms_l, "arms_l", dtype=torch.int32, shape=(H, W)),
+                            _need(arms_r, "arms_r", dtype=torch.int32, shape=(H, W)), H, W, D, int(L1), int(iters),
+                            _stream()), "sde_cbca_pair")
+    return cv_l, cv_r
+
+
 def lr_check(disp_l, disp_r, lrc_l=None, lrc_r=None):
     H, W = disp_l.shape
     if lrc_l is None:

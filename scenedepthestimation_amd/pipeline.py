@@ -128,7 +128,6 @@ class StereoMatcher:
         )
         if self.cbca_iters > 0:
             self.sgm_bufs["arms"] = [torch.empty((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
-            self.sgm_bufs["cbca_tmp"] = torch.empty((H, W, D), dtype=torch.float32, device=dev)
 
     def cbca(self, cv_l, cv_r, img_l, img_r):
         """Cross-based aggregation of the L/R [H,W,D] volumes in place (build-defined).
@@ -141,8 +140,9 @@ class StereoMatcher:
         for k, img in enumerate((img_l, img_r)):
             ops.preprocess_u8(img, P, out=self.img_pad[k], stats=self.stats[k])
             ops.cbca_arms(self.img_pad[k][P:P + H, P:P + W], self.cbca_L1, self.cbca_tau, out=b["arms"][k])
-        ops.cbca(cv_l, b["arms"][0], b["arms"][1], "left", self.cbca_L1, self.cbca_iters, tmp=b["cbca_tmp"])
-        ops.cbca(cv_r, b["arms"][1], b["arms"][0], "right", self.cbca_L1, self.cbca_iters, tmp=b["cbca_tmp"])
+        # both sides per launch; the SGM S buffers (written later, overwrite mode) are the scratch
+        ops.cbca_pair(cv_l, cv_r, b["arms"][0], b["arms"][1], self.cbca_L1, self.cbca_iters,
+                      tmp_l=b["S"][0], tmp_r=b["S"][1])
         return cv_l, cv_r
 
     def sgm_path(self, fl=None, fr=None, img_l=None, img_r=None, timings=None, post=True):

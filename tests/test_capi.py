@@ -106,6 +106,8 @@ def test_argument_validation_without_gpu():
     assert lib.sde_cv_wta_split(1, 1, N, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 1 << 20, N) == ERR
     assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
     assert lib.sde_tower_packed_floats(0, 64) == -1
+    assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 4, 8, 14, 1, N) == ERR                          # aliased buffers
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 4, 8, 33, 1, N) == ERR                          # L1 > 32
 
 
 def test_ops_refuse_cpu_tensors():

@@ -278,6 +278,23 @@ def test_sgm_8path_bit_exact(gpu, oracle, H, W, D):
     assert np.array_equal(host(ops.wta(dev(ref), "HWD", "d0")), oracle.wta_sgm(ref))
 
 
+@pytest.mark.parametrize("H,W,D,L1,iters", [(23, 61, 40, 14, 2), (40, 33, 130, 16, 1), (70, 12, 7, 32, 2),
+                                             (3, 2, 16, 14, 1), (16, 96, 192, 14, 3)])
+def test_cbca_pair_bit_exact(gpu, oracle, H, W, D, L1, iters):
+    """Both volumes of a pair in one launch per pass == the oracle's per-side aggregation."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(7 * H + W + D)
+    il, ir = _cbca_images(rng, H, W), _cbca_images(rng, H, W)
+    al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
+    cl = rng.standard_normal((H, W, D)).astype(np.float32)
+    cr = rng.standard_normal((H, W, D)).astype(np.float32)
+    want_l, want_r = oracle.cbca(cl, al, ar, "left", iters), oracle.cbca(cr, ar, al, "right", iters)
+    gl, gr = dev(cl), dev(cr)
+    ops.cbca_pair(gl, gr, dev(al.view(np.int32)), dev(ar.view(np.int32)), L1, iters)
+    assert host(gl).tobytes() == want_l.tobytes()
+    assert host(gr).tobytes() == want_r.tobytes()
+
+
 @pytest.mark.parametrize("H,W,D", [(33, 70, 97), (19, 41, 192), (5, 130, 64), (70, 9, 300), (2, 50, 64)])
 def test_sgm_8path_pair_bit_exact(gpu, oracle, H, W, D):
     """Both sides per launch; overwrite mode ignores S's contents, accumulate mode adds to them."""
@@ -329,7 +346,8 @@ def test_cbca_arms_bit_exact(gpu, oracle, L1, tau):
 
 @pytest.mark.parametrize("H,W,D,L1,iters,side", [(23, 61, 40, 14, 2, "left"), (40, 33, 100, 16, 1, "right"),
                                                  (9, 130, 64, 20, 1, "left"), (70, 12, 7, 32, 2, "right"),
-                                                 (5, 5, 3, 14, 0, "left")])
+                                                 (5, 5, 3, 14, 0, "left"), (16, 96, 192, 14, 2, "left"),
+                                                 (12, 300, 256, 14, 1, "left")])
 def test_cbca_bit_exact(gpu, oracle, H, W, D, L1, iters, side):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(H * W + D)
