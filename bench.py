@@ -363,14 +363,16 @@ def main():
         # per side: UD+DU pass reads C, writes S (8 B/voxel); 5 passes read C, S and write S (12 B);
         # the last pass (WTA fused) reads C, S (8 B) and writes 4 B per pixel
         sgm_bytes = 2 * (76.0 * vox + 4.0 * H * W)
-        tmp = b["cbca_tmp"]
+        # one CBCA iteration of both sides (sde_cbca_pair: 2 launches; S buffers as scratch, as in sgm_path)
         e0.record()
-        ops.cbca(b["cv"][0], b["arms"][0], b["arms"][1], "left", CBCA_L1, 1, tmp=tmp)
+        ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], CBCA_L1, 1, tmp_l=b["S"][0],
+                      tmp_r=b["S"][1])
         e1.record()
         torch.cuda.synchronize()
         cb_ms = e0.elapsed_time(e1)
-        stages["cbca_iter_ms"] = cb_ms
-        stages["cbca_iter_hbm_GBs"] = 16.0 * vox / (cb_ms * 1e-3) / 1e9     # 2 passes x (read + write) x 4 B
+        stages["cbca_pair_iter_ms"] = cb_ms
+        # 2 sides x 2 passes x (read + write) x 4 B
+        stages["cbca_pair_iter_hbm_GBs"] = 2 * 16.0 * vox / (cb_ms * 1e-3) / 1e9
         stages["sgm_pair_ms"] = sgm_ms
         ach = sgm_bytes / (sgm_ms * 1e-3) / 1e9
         roof = {"kernel": "sgm_scan_kernel (8-path SGM + WTA, both sides, 7 launches: DU folded into UD, WTA "

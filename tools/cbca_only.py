@@ -32,8 +32,12 @@ def main(H=1024, W=1024, D=192, L1=14, reps=5):
     def single():
         ops.cbca(cl, al, ar, "left", L1, 1, tmp=tl)
         ops.cbca(cr, ar, al, "right", L1, 1, tmp=tr)
-    ms_s = timed(single, reps)
-    ms_p = timed(lambda: ops.cbca_pair(cl, cr, al, ar, L1, 1, tmp_l=tl, tmp_r=tr), reps)
+    ss, ps = [], []
+    for _ in range(5):      # interleaved: the clock drifts over a run
+        ss.append(timed(single, reps))
+        ps.append(timed(lambda: ops.cbca_pair(cl, cr, al, ar, L1, 1, tmp_l=tl, tmp_r=tr), reps))
+    ms_s, ms_p = sorted(ss)[2], sorted(ps)[2]
+    print("single:", " ".join(f"{t:.3f}" for t in ss), " pair:", " ".join(f"{t:.3f}" for t in ps))
     gb = 2 * 16 * H * W * D / 1e6     # GB * 1e3: GB/s from ms
     print(f"one iteration, both sides: two single calls {ms_s:.3f} ms ({gb / ms_s:.0f} GB/s), "
           f"pair {ms_p:.3f} ms ({gb / ms_p:.0f} GB/s)", flush=True)
