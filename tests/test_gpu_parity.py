@@ -295,6 +295,30 @@ def test_cbca_pair_bit_exact(gpu, oracle, H, W, D, L1, iters):
     assert host(gr).tobytes() == want_r.tobytes()
 
 
+def test_cbca_pair_bench_width_bit_exact(gpu, oracle):
+    """A band of rows at the benchmark's width and D (1024 x 192): every x - d / x + d edge regime."""
+    test_cbca_pair_bit_exact(gpu, oracle, 24, 1024, 192, 14, 2)
+
+
+def test_cbca_pair_config3_identity(gpu):
+    """Middlebury-2014 scale (2000 x 3000 x 256: 6 GB per volume, the V pass's offsets beyond 32 bits):
+    with zero arms every support is the pixel itself, and for small-integer costs the fp64 prefix
+    differences are exact, so both volumes must come back unchanged bit for bit -- any misaddressed
+    row, column or disparity changes a value."""
+    from scenedepthestimation_amd import ops
+    H, W, D = 2000, 3000, 256
+    y = torch.arange(H, device="cuda").view(H, 1, 1)
+    x = torch.arange(W, device="cuda").view(1, W, 1)
+    d = torch.arange(D, device="cuda").view(1, 1, D)
+    cl = ((7 * y + 3 * x + d) % 13).float()
+    cr = ((5 * y + 11 * x + 2 * d) % 17).float()
+    arms = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+    gl, gr = cl.clone(), cr.clone()
+    ops.cbca_pair(gl, gr, arms, arms, 14, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(gl, cl) and torch.equal(gr, cr)
+
+
 @pytest.mark.parametrize("H,W,D", [(33, 70, 97), (19, 41, 192), (5, 130, 64), (70, 9, 300), (2, 50, 64)])
 def test_sgm_8path_pair_bit_exact(gpu, oracle, H, W, D):
     """Both sides per launch; overwrite mode ignores S's contents, accumulate mode adds to them."""
