@@ -232,9 +232,12 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
 // first-min disparity (rule of WTA_and_SupixelRefinement_kernel) goes to sd.disp instead, and
 // the pixels this direction never visits (its lines stop one short) take the WTA of the S
 // already in memory.
-template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA>
+template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA, int DC>
 __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
+    // DC != 0: D == DC == 64 * DPL is a compile-time constant -- every lane's disparities are
+    // valid, so the per-disparity range guards and the pixel index's division fold away
+    if (DC) D = DC;
     const SgmSide sd = blockIdx.y ? s1 : s0;
     PathGeom g;
     g.dr = c_dir_dr[dir]; g.dc = c_dir_dc[dir]; g.ch = c_dir_ch[dir];
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     const int nlen = (g.dc != 0 && g.dr == 0) ? W : H;
     g.n = nlen - 1 > 2 ? nlen - 1 : 2;
     const int line = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;      // one wave per block: lane < 64 known to the compiler
     const int dbase = lane * DPL;
     const double INF = __builtin_inf();
     // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block)
@@ -398,7 +401,11 @@ static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, i
     const bool horiz = (dir == 2 || dir == 3);
     const int nlines = horiz ? H : W;
     constexpr int PF = DPL <= 4 ? 8 : 4;
-    sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
+    if (VEC && D == 64 * DPL)
+        sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, 64 * DPL><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D,
+                                                                                                   dir);
+    else
+        sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, 0><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
 }
 
 // mode: 0 accumulate, 1 first (S := 0 + L), 2 first + DU fold, 3 accumulate + DU fold,
