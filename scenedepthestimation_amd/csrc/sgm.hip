@@ -232,7 +232,7 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
 // first-min disparity (rule of WTA_and_SupixelRefinement_kernel) goes to sd.disp instead, and
 // the pixels this direction never visits (its lines stop one short) take the WTA of the S
 // already in memory.
-template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA, int DC>
+template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA, int DC, int DIRC>
 __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
     // DC != 0: D == DC == 64 * DPL is a compile-time constant -- every lane's disparities are
@@ -240,7 +240,15 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     if (DC) D = DC;
     const SgmSide sd = blockIdx.y ? s1 : s0;
     PathGeom g;
-    g.dr = c_dir_dr[dir]; g.dc = c_dir_dc[dir]; g.ch = c_dir_ch[dir];
+    // DIRC >= 0: the direction is a compile-time constant (the walker's steps, wrap tests and the
+    // penalty channel fold); the pair path's seven launches use these
+    constexpr int kdr[8] = {+1, -1, 0, 0, +1, -1, +1, -1}, kdc[8] = {0, 0, +1, -1, +1, +1, -1, -1},
+                  kch[8] = {2, 0, 6, 4, 10, 12, 8, 14};
+    if (DIRC >= 0) {
+        g.dr = kdr[DIRC & 7]; g.dc = kdc[DIRC & 7]; g.ch = kch[DIRC & 7];
+    } else {
+        g.dr = c_dir_dr[dir]; g.dc = c_dir_dc[dir]; g.ch = c_dir_ch[dir];
+    }
     g.H = H; g.W = W;
     const int nlen = (g.dc != 0 && g.dr == 0) ? W : H;
     g.n = nlen - 1 > 2 ? nlen - 1 : 2;
@@ -401,11 +409,38 @@ static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, i
     const bool horiz = (dir == 2 || dir == 3);
     const int nlines = horiz ? H : W;
     constexpr int PF = DPL <= 4 ? 8 : 4;
-    if (VEC && D == 64 * DPL)
-        sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, 64 * DPL><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D,
-                                                                                                   dir);
-    else
-        sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, 0><<<dim3(nlines, nsides), 64, 0, st>>>(a, b, H, W, D, dir);
+    const dim3 grid(nlines, nsides);
+#define SDE_SGM_LAUNCH(DC, DIRC) sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, DC, DIRC><<<grid, 64, 0, st>>>(a, b, H, W, D, dir)
+    if constexpr (!VEC) {
+        SDE_SGM_LAUNCH(0, -1);
+    } else {
+    if (D != 64 * DPL) {
+        SDE_SGM_LAUNCH(0, -1);
+        return;
+    }
+    constexpr int DC = 64 * DPL;
+    // compile-time directions for the combinations sde_sgm_8path_wta_pair launches (UD + DU fold,
+    // the five middle directions, DU-RL + WTA); any other stays generic
+    if constexpr (DU) {
+        if (dir == 0) SDE_SGM_LAUNCH(DC, 0);
+        else SDE_SGM_LAUNCH(DC, -1);
+    } else if constexpr (WTA) {
+        if (dir == 7) SDE_SGM_LAUNCH(DC, 7);
+        else SDE_SGM_LAUNCH(DC, -1);
+    } else if constexpr (!FIRST) {
+        switch (dir) {
+        case 2: SDE_SGM_LAUNCH(DC, 2); break;
+        case 3: SDE_SGM_LAUNCH(DC, 3); break;
+        case 4: SDE_SGM_LAUNCH(DC, 4); break;
+        case 5: SDE_SGM_LAUNCH(DC, 5); break;
+        case 6: SDE_SGM_LAUNCH(DC, 6); break;
+        default: SDE_SGM_LAUNCH(DC, -1); break;
+        }
+    } else {
+        SDE_SGM_LAUNCH(DC, -1);
+    }
+    }
+#undef SDE_SGM_LAUNCH
 }
 
 // mode: 0 accumulate, 1 first (S := 0 + L), 2 first + DU fold, 3 accumulate + DU fold,
