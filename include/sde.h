@@ -324,6 +324,8 @@ int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *ar
  */
 int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_r, const uint32_t *arms_l,
                   const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *stream);
+/* sde_cbca / sde_cbca_pair shape limits (32-bit scan offsets, refused with SDE_ERR_ARG):
+ * H, W <= 65535, 4*H*W < 2^31 and (3R + 18) * 4*W*D < 2^31 with R = 15 (L1 <= 16) or 31. */
 
 /* is_error_match_kernel (process_functional.py:977-1000): lrc_l/lrc_r u8 [H][W], caller-zeroed. */
 int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,
@@ -331,7 +333,7 @@ int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t
 
 /* LRC_kernel left output (process_functional.py:1003-1088).  Two linear scans instead of
  * the reference's per-pixel walks; `out` doubles as scratch, so out != disp_l.  Requires
- * H < 65535 and W <= 4096. */
+ * H < 65535 and W < 65535 (16-bit row / column indices; the row pass keeps 2 B per column in LDS). */
 int sde_lrc_fill(const float *disp_l, const uint8_t *lrc_l, int H, int W, float *out, void *stream);
 
 /* Median_Filter_kernel (process_functional.py:840-879): 5x5 median of src into the interior of dst. */

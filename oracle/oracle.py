@@ -33,6 +33,8 @@ def lib():
     if _lib is None:
         build()
         L = ctypes.CDLL(_LIB_PATH)
+        L.sdeo_set_threads.argtypes = [ctypes.c_int]
+        L.sdeo_get_threads.restype = ctypes.c_int
         L.sdeo_np_sum_f32.restype = ctypes.c_float
         L.sdeo_np_sum_f32.argtypes = [_f32p, ctypes.c_long]
         L.sdeo_cost_volume_dhw.argtypes = [_f32p, _f32p] + [ctypes.c_int] * 4 + [_f32p]
@@ -57,7 +59,17 @@ def lib():
                                      _u32p]
         L.sdeo_cbca.argtypes = [_f32p, _f32p, _u32p, _u32p] + [ctypes.c_int] * 5
         _lib = L
+        L.sdeo_set_threads(int(os.environ.get("SDE_ORACLE_THREADS", min(16, os.cpu_count() or 1))))
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads for the oracle's parallel loops (bit-identical results for any count)."""
+    lib().sdeo_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(lib().sdeo_get_threads())
 
 
 def _p(a, t=_f32p):

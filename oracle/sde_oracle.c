@@ -25,6 +25,12 @@
 
 #define EXPORT __attribute__((visibility("default")))
 
+/* OpenMP over independent lines / rows / pixels (bit-identical to a serial run: no loop
+ * below reorders any per-element arithmetic).  Thread count: sdeo_set_threads (default 1). */
+static int g_threads = 1;
+EXPORT void sdeo_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+EXPORT int sdeo_get_threads(void) { return g_threads; }
+
 /* ------------------------------------------------------------------------ */
 /* NumPy float32 add.reduce: result = 0.0f + pairwise_sum(a, n).             */
 /* numpy/_core/src/umath/loops_utils.h.src (pairwise_sum, PW_BLOCKSIZE 128); */
@@ -72,17 +78,21 @@ static float np_neg_dot(const float *l, const float *r, int C, float *tmp)
 EXPORT void sdeo_cost_volume_dhw(const float *fl, const float *fr, int H, int W, int C, int D,
                                  float *out)
 {
-    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
-    for (int d = 0; d < D; d++)
+#pragma omp parallel num_threads(g_threads)
+    {
+        float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+#pragma omp for schedule(static)
         for (int y = 0; y < H; y++)
-            for (int x = 0; x < W; x++) {
-                float *o = out + ((size_t)d * H + y) * W + x;
-                if (x >= d)
-                    *o = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
-                else
-                    *o = -0.0f;   /* np.zeros then `-1 *` */
-            }
-    free(tmp);
+            for (int d = 0; d < D; d++)
+                for (int x = 0; x < W; x++) {
+                    float *o = out + ((size_t)d * H + y) * W + x;
+                    if (x >= d)
+                        *o = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
+                    else
+                        *o = -0.0f;   /* np.zeros then `-1 *` */
+                }
+        free(tmp);
+    }
 }
 
 /*
@@ -94,24 +104,31 @@ EXPORT void sdeo_cost_volume_dhw(const float *fl, const float *fr, int H, int W,
 EXPORT void sdeo_cost_volume_hwd(const float *fl, const float *fr, int H, int W, int C, int D,
                                  float invalid, float *outl, float *outr)
 {
-    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
-    size_t n = (size_t)H * W * D;
-    if (outl) for (size_t i = 0; i < n; i++) outl[i] = invalid;
-    if (outr) for (size_t i = 0; i < n; i++) outr[i] = invalid;
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++)
-            for (int d = 0; d < D && d <= x; d++) {
-                float c = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
-                if (outl) outl[((size_t)y * W + x) * D + d] = c;
-                if (outr) outr[((size_t)y * W + x - d) * D + d] = c;
-            }
-    free(tmp);
+#pragma omp parallel num_threads(g_threads)
+    {
+        float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+        /* row y's voxels (left and right) are written by row y's thread only */
+#pragma omp for schedule(static)
+        for (int y = 0; y < H; y++) {
+            const size_t r0 = (size_t)y * W * D, rn = (size_t)W * D;
+            if (outl) for (size_t i = 0; i < rn; i++) outl[r0 + i] = invalid;
+            if (outr) for (size_t i = 0; i < rn; i++) outr[r0 + i] = invalid;
+            for (int x = 0; x < W; x++)
+                for (int d = 0; d < D && d <= x; d++) {
+                    float c = np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp);
+                    if (outl) outl[((size_t)y * W + x) * D + d] = c;
+                    if (outr) outr[((size_t)y * W + x - d) * D + d] = c;
+                }
+        }
+        free(tmp);
+    }
 }
 
 /* WTA1 (process_functional.py:96-113): first d with cost < running min (init +inf). */
 EXPORT int sdeo_wta1_dhw(const float *cv, int D, int H, int W, float *disp)
 {
     int bad = 0;
+#pragma omp parallel for num_threads(g_threads) reduction(+ : bad) schedule(static)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             float best = INFINITY;
@@ -130,6 +147,7 @@ EXPORT int sdeo_wta1_dhw(const float *cv, int D, int H, int W, float *disp)
 EXPORT int sdeo_wta_hwd(const float *cv, int H, int W, int D, float *disp)
 {
     int bad = 0;
+#pragma omp parallel for num_threads(g_threads) reduction(+ : bad) schedule(static)
     for (size_t p = 0; p < (size_t)H * W; p++) {
         float best = INFINITY;
         int arg = -1;
@@ -149,6 +167,7 @@ EXPORT int sdeo_wta_hwd(const float *cv, int H, int W, int D, float *disp)
  */
 EXPORT void sdeo_wta_sgm_hwd(const float *S, int H, int W, int D, float *disp)
 {
+#pragma omp parallel for num_threads(g_threads) schedule(static)
     for (size_t p = 0; p < (size_t)H * W; p++) {
         float m = S[p * D];
         int arg = 0;
@@ -168,20 +187,25 @@ EXPORT void sdeo_wta_sgm_hwd(const float *S, int H, int W, int D, float *disp)
 EXPORT void sdeo_cv_wta_shard(const float *fl, const float *fr, int H, int W, int C, int d0, int d1,
                               float *minv, int32_t *argmin)
 {
-    float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
-    for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++) {
-            float best = INFINITY;
-            int arg = -1;
-            for (int d = d0; d < d1; d++) {
-                float v = (x >= d) ? np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C, tmp)
-                                   : -0.0f;
-                if (v < best) { best = v; arg = d; }
+#pragma omp parallel num_threads(g_threads)
+    {
+        float *tmp = (float *)malloc(sizeof(float) * (C > 0 ? C : 1));
+#pragma omp for schedule(static)
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) {
+                float best = INFINITY;
+                int arg = -1;
+                for (int d = d0; d < d1; d++) {
+                    float v = (x >= d) ? np_neg_dot(fl + ((size_t)y * W + x) * C, fr + ((size_t)y * W + x - d) * C, C,
+                                                    tmp)
+                                       : -0.0f;
+                    if (v < best) { best = v; arg = d; }
+                }
+                minv[(size_t)y * W + x] = best;
+                argmin[(size_t)y * W + x] = arg;
             }
-            minv[(size_t)y * W + x] = best;
-            argmin[(size_t)y * W + x] = arg;
-        }
-    free(tmp);
+        free(tmp);
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -201,6 +225,7 @@ EXPORT void sdeo_sgm_penalties(const uint8_t *img, int H, int W, double P1, doub
         {-1, 0, 2}, {+1, 0, 2}, {0, -1, 4}, {0, +1, 6},
         {+1, -1, 8}, {+1, +1, 10}, {-1, +1, 12}, {-1, -1, 14},
     };
+#pragma omp parallel for num_threads(g_threads) schedule(static)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             float *p = pen + ((size_t)y * W + x) * 16;
@@ -224,12 +249,43 @@ EXPORT void sdeo_sgm_penalties(const uint8_t *img, int H, int W, double P1, doub
 
 /* ------------------------------------------------------------------------ */
 /* 8-path SGM (process_functional.py:265-797, launch order :1166-1203).      */
+/* The reference runs one warp per scanline: lane j of the 32 holds the 4   */
+/* disparities 4j..4j+3 (D = 128).  Its arithmetic, restated exactly so     */
+/* that non-finite costs propagate as they do there:                        */
+/*  - every `min(a, b)` is Numba's (= Python's) binary min: b if b < a else  */
+/*    a (numba cpython/builtins.py do_minmax: select(v < acc, v, acc)), so a */
+/*    NaN first argument sticks and a NaN second argument is ignored;       */
+/*  - c_k += min(min(L(d-1) + P1, L(d)), min(L(d+1) + P1, mcP2)) - mc with  */
+/*    L(d-1) := L(d) at d = 0 and L(d+1) := L(d) at d = D-1 (:300-303,        */
+/*    :306-320);                                                            */
+/*  - the minimum is per lane: m = min(min(c1, c2), min(c3, c4)), then       */
+/*    m = min(m, shfl_xor(m, k)) for k = 1, 2, 4, 8, 16 (:329-338) -- with  */
+/*    NaN present, lanes can end with different minima, and each lane uses */
+/*    its own m and m + P2 at the next step.                                 */
+/* For finite costs every lane's m is the global minimum and the chain's   */
+/* value is the plain minimum, so the result does not depend on the        */
+/* grouping.  Generic D (the reference has D = 128 only): lanes of 4        */
+/* (missing disparities of the last lane act as +inf, which the binary min  */
+/* ignores), the butterfly over the next power of two of ceil(D/4) lanes    */
+/* with the padding lanes at +inf.                                          */
 /* ------------------------------------------------------------------------ */
+static inline double pymin(double a, double b) { return b < a ? b : a; }
+
 typedef struct {
     double *L;      /* path cost of the previous pixel, fp64 (Numba-unified) */
     double *Ln;
-    double m, mP2;
+    double *m;      /* per reference lane (4 disparities): min_cost */
+    double *mP2;    /* per reference lane: min_cost + P2 */
+    double *v;      /* butterfly scratch, nlp entries */
+    int nlp;        /* reference lanes, rounded up to a power of two */
 } sgm_state;
+
+static int sgm_lanes_pow2(int D)
+{
+    int nl = (D + 3) / 4, p = 1;
+    while (p < nl) p <<= 1;
+    return p;
+}
 
 /* One SGM_Interation (:265-343) at pixel (r,c). */
 static void sgm_step(const float *C, float *S, sgm_state *st, int D, int restart, double P1, double P2,
@@ -240,90 +296,121 @@ static void sgm_step(const float *C, float *S, sgm_state *st, int D, int restart
         for (int d = 0; d < D; d++) Ln[d] = (double)C[d];
     } else {
         for (int d = 0; d < D; d++) {
-            double b = L[d];
-            if (d > 0) { double t = L[d - 1] + P1; if (t < b) b = t; }
-            if (d < D - 1) { double t = L[d + 1] + P1; if (t < b) b = t; }
-            if (st->mP2 < b) b = st->mP2;
-            Ln[d] = (double)C[d] + (b - st->m);
+            const double self = L[d];
+            const double lft = d > 0 ? L[d - 1] : self, rgt = d < D - 1 ? L[d + 1] : self;
+            const double m1 = pymin(lft + P1, self);
+            const double m2 = pymin(rgt + P1, st->mP2[d >> 2]);
+            Ln[d] = (double)C[d] + (pymin(m1, m2) - st->m[d >> 2]);
         }
     }
     for (int d = 0; d < D; d++) S[d] = (float)((double)S[d] + Ln[d]);
     if (calc_min) {
-        double m = Ln[0];
-        for (int d = 1; d < D; d++) if (Ln[d] < m) m = Ln[d];
-        st->m = m;
-        st->mP2 = m + P2;
+        double *v = st->v;
+        const int nlp = st->nlp;
+        for (int j = 0; j < nlp; j++) {
+            double c[4];
+            for (int k = 0; k < 4; k++) c[k] = 4 * j + k < D ? Ln[4 * j + k] : INFINITY;
+            v[j] = pymin(pymin(c[0], c[1]), pymin(c[2], c[3]));
+        }
+        for (int k = 1; k < nlp; k <<= 1) {
+            /* simultaneous exchange: m_j = min(m_j, m_{j^k}); each pair computed from the old values */
+            for (int j = 0; j < nlp; j++) {
+                const int o = j ^ k;
+                if (o < j) continue;
+                const double a = v[j], b = v[o];
+                v[j] = pymin(a, b);
+                v[o] = pymin(b, a);
+            }
+        }
+        for (int j = 0; j < nlp; j++) {
+            st->m[j] = v[j];
+            st->mP2[j] = v[j] + P2;
+        }
     }
     st->L = Ln;
     st->Ln = L;
+}
+
+static void sgm_state_init(sgm_state *st, double *buf, int D)
+{
+    const int nlp = sgm_lanes_pow2(D);
+    st->L = buf;
+    st->Ln = buf + D;
+    st->m = buf + 2 * D;
+    st->mP2 = buf + 2 * D + nlp;
+    st->v = buf + 2 * D + 2 * nlp;
+    st->nlp = nlp;
+    for (int d = 0; d < D; d++) st->L[d] = 1.0;     /* old_values = 1.0 (:359-364); unused at restart */
+    for (int j = 0; j < nlp; j++) st->m[j] = st->mP2[j] = 1.0;
 }
 
 static inline int sgm_nsteps(int n) { return n - 1 > 2 ? n - 1 : 2; }
 
 enum { SGM_UD = 0, SGM_DU, SGM_LR, SGM_RL, SGM_UDLR, SGM_DULR, SGM_UDRL, SGM_DURL };
 
-/* One direction over one side: cv/pen/S are [H][W][D], [H][W][16], [H][W][D]. */
+/* One direction over one side: cv/pen/S are [H][W][D], [H][W][16], [H][W][D].  Lines are
+ * independent (each pixel is visited once per direction), so they run in parallel. */
 EXPORT void sdeo_sgm_direction(const float *cv, const float *pen, int H, int W, int D, int dir,
                                float *S)
 {
-    double *b0 = (double *)malloc(sizeof(double) * D), *b1 = (double *)malloc(sizeof(double) * D);
 #define CV(r, c) (cv + ((size_t)(r) * W + (c)) * D)
 #define SS(r, c) (S + ((size_t)(r) * W + (c)) * D)
 #define PEN(r, c, ch) ((double)pen[((size_t)(r) * W + (c)) * 16 + (ch)])
-    if (dir == SGM_UD || dir == SGM_DU) {
-        int n = sgm_nsteps(H);
-        for (int c = 0; c < W; c++) {
-            sgm_state st = {b0, b1, 1.0, 1.0};
-            for (int k = 0; k < n; k++) {
-                int r = dir == SGM_UD ? k : H - 1 - k;
-                double P1 = 0.0, P2;
-                if (dir == SGM_UD) { if (r - 1 >= 0) P1 = PEN(r - 1, c, 2); P2 = PEN(r, c, 3); }
-                else               { if (r + 1 < H)  P1 = PEN(r + 1, c, 0); P2 = PEN(r, c, 1); }
-                sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
-            }
-        }
-    } else if (dir == SGM_LR || dir == SGM_RL) {
-        int n = sgm_nsteps(W);
-        for (int r = 0; r < H; r++) {
-            sgm_state st = {b0, b1, 1.0, 1.0};
-            for (int k = 0; k < n; k++) {
-                int c = dir == SGM_LR ? k : W - 1 - k;
-                double P1 = 0.0, P2;
-                if (dir == SGM_LR) { if (c - 1 >= 0) P1 = PEN(r, c - 1, 6); P2 = PEN(r, c, 7); }
-                else               { if (c + 1 < W)  P1 = PEN(r, c + 1, 4); P2 = PEN(r, c, 5); }
-                sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
-            }
-        }
-    } else {
-        int n = sgm_nsteps(H);
-        int down = (dir == SGM_UDLR || dir == SGM_UDRL);
-        int right = (dir == SGM_UDLR || dir == SGM_DULR);
-        int p1ch = dir == SGM_UDLR ? 10 : dir == SGM_DULR ? 12 : dir == SGM_UDRL ? 8 : 14;
-        for (int c0 = 0; c0 < W; c0++) {
-            sgm_state st = {b0, b1, 1.0, 1.0};
-            int c = c0;
-            for (int k = 0; k < n; k++) {
-                int r = down ? k : H - 1 - k;
-                int restart = (k == 0);
-                if (k > 0) {
-                    c += right ? 1 : -1;
-                    if (right && c >= W) { c = 0; restart = 1; }
-                    if (!right && c < 0) { c = W - 1; restart = 1; }
+    const int nlp = sgm_lanes_pow2(D);
+    const int nlines = (dir == SGM_LR || dir == SGM_RL) ? H : W;
+#pragma omp parallel num_threads(g_threads)
+    {
+        double *buf = (double *)malloc(sizeof(double) * (2 * (size_t)D + 3 * (size_t)nlp));
+#pragma omp for schedule(dynamic, 16)
+        for (int line = 0; line < nlines; line++) {
+            sgm_state st;
+            sgm_state_init(&st, buf, D);
+            if (dir == SGM_UD || dir == SGM_DU) {
+                const int n = sgm_nsteps(H), c = line;
+                for (int k = 0; k < n; k++) {
+                    int r = dir == SGM_UD ? k : H - 1 - k;
+                    double P1 = 0.0, P2;
+                    if (dir == SGM_UD) { if (r - 1 >= 0) P1 = PEN(r - 1, c, 2); P2 = PEN(r, c, 3); }
+                    else               { if (r + 1 < H)  P1 = PEN(r + 1, c, 0); P2 = PEN(r, c, 1); }
+                    sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
                 }
-                int pr = down ? r - 1 : r + 1;
-                int pc = right ? c - 1 : c + 1;
-                double P1 = 0.0;
-                if (pr >= 0 && pr < H && pc >= 0 && pc < W) P1 = PEN(pr, pc, p1ch);
-                double P2 = PEN(r, c, p1ch + 1);
-                sgm_step(CV(r, c), SS(r, c), &st, D, restart, P1, P2, k < n - 1);
+            } else if (dir == SGM_LR || dir == SGM_RL) {
+                const int n = sgm_nsteps(W), r = line;
+                for (int k = 0; k < n; k++) {
+                    int c = dir == SGM_LR ? k : W - 1 - k;
+                    double P1 = 0.0, P2;
+                    if (dir == SGM_LR) { if (c - 1 >= 0) P1 = PEN(r, c - 1, 6); P2 = PEN(r, c, 7); }
+                    else               { if (c + 1 < W)  P1 = PEN(r, c + 1, 4); P2 = PEN(r, c, 5); }
+                    sgm_step(CV(r, c), SS(r, c), &st, D, k == 0, P1, P2, k < n - 1);
+                }
+            } else {
+                const int n = sgm_nsteps(H);
+                const int down = (dir == SGM_UDLR || dir == SGM_UDRL);
+                const int right = (dir == SGM_UDLR || dir == SGM_DULR);
+                const int p1ch = dir == SGM_UDLR ? 10 : dir == SGM_DULR ? 12 : dir == SGM_UDRL ? 8 : 14;
+                int c = line;
+                for (int k = 0; k < n; k++) {
+                    int r = down ? k : H - 1 - k;
+                    int restart = (k == 0);
+                    if (k > 0) {
+                        c += right ? 1 : -1;
+                        if (right && c >= W) { c = 0; restart = 1; }
+                        if (!right && c < 0) { c = W - 1; restart = 1; }
+                    }
+                    int pr = down ? r - 1 : r + 1;
+                    int pc = right ? c - 1 : c + 1;
+                    double P1 = 0.0;
+                    if (pr >= 0 && pr < H && pc >= 0 && pc < W) P1 = PEN(pr, pc, p1ch);
+                    double P2 = PEN(r, c, p1ch + 1);
+                    sgm_step(CV(r, c), SS(r, c), &st, D, restart, P1, P2, k < n - 1);
+                }
             }
         }
+        free(buf);
     }
 #undef CV
 #undef SS
 #undef PEN
-    free(b0);
-    free(b1);
 }
 
 /* All 8 directions in the reference launch order; S is accumulated (caller zeroes it). */
@@ -342,6 +429,7 @@ static inline int u8cast(double v) { long long t = (long long)v; return (int)(t 
 
 EXPORT void sdeo_lr_check(const float *dl, const float *dr, int H, int W, uint8_t *lrcl, uint8_t *lrcr)
 {
+#pragma omp parallel for num_threads(g_threads) schedule(static)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             double ld = dl[(size_t)y * W + x];
@@ -363,6 +451,7 @@ EXPORT void sdeo_lr_check(const float *dl, const float *dr, int H, int W, uint8_
 
 EXPORT void sdeo_lrc_fill(const float *dl, const uint8_t *lrcl, int H, int W, float *out)
 {
+#pragma omp parallel for num_threads(g_threads) schedule(dynamic, 4)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             size_t p = (size_t)y * W + x;
@@ -391,7 +480,8 @@ EXPORT void sdeo_lrc_fill(const float *dl, const uint8_t *lrcl, int H, int W, fl
 /* 5x5 median of the interior (2-px border of `out` untouched): partial selection sort to the 13th. */
 EXPORT void sdeo_median5(const float *in, int H, int W, float *out)
 {
-    for (int y = 2; y + 2 < H; y++)
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+    for (int y = 2; y < H - 2; y++)
         for (int x = 2; x + 2 < W; x++) {
             float w[25];
             for (int i = -2; i <= 2; i++)
@@ -423,6 +513,7 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
         int ho = h - 2, wo = w - 2;
         double *nxt = (double *)malloc(sizeof(double) * (size_t)ho * wo * nf);
         const float *Wt = weights[l], *B = biases[l];
+#pragma omp parallel for num_threads(g_threads) schedule(static)
         for (int y = 0; y < ho; y++)
             for (int x = 0; x < wo; x++)
                 for (int n = 0; n < nf; n++) {
@@ -442,6 +533,7 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
         w = wo;
         cin = nf;
     }
+#pragma omp parallel for num_threads(g_threads) schedule(static)
     for (size_t p = 0; p < (size_t)h * w; p++) {
         double ss = 0.0;
         for (int n = 0; n < nf; n++) ss += cur[p * nf + n] * cur[p * nf + n];
@@ -478,6 +570,7 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
 EXPORT void sdeo_cbca_arms(const float *img, long pitch, int H, int W, int L1, float tau, uint32_t *arms)
 {
     static const int dys[4] = {0, 0, -1, 1}, dxs[4] = {-1, 1, 0, 0};
+#pragma omp parallel for num_threads(g_threads) schedule(static)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             const float c = img[(size_t)y * pitch + x];
@@ -512,25 +605,32 @@ static inline void cbca_support(const uint32_t *ref, const uint32_t *oth, int W,
 EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
                             int D, int side)
 {
-    double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1));   /* P[x + 1] = prefix through x */
-    for (int y = 0; y < H; y++)
-        for (int d = 0; d < D; d++) {
-            P[0] = 0.0;
-            for (int x = 0; x < W; x++) P[x + 1] = P[x] + (double)src[((size_t)y * W + x) * D + d];
-            for (int x = 0; x < W; x++) {
-                int a[4];
-                cbca_support(ref, oth, W, y, x, d, side, a);
-                dst[((size_t)y * W + x) * D + d] = (float)(P[x + a[1] + 1] - P[x - a[0]]);
+#pragma omp parallel num_threads(g_threads)
+    {
+        double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1));   /* P[x + 1] = prefix through x */
+#pragma omp for schedule(static)
+        for (int y = 0; y < H; y++)
+            for (int d = 0; d < D; d++) {
+                P[0] = 0.0;
+                for (int x = 0; x < W; x++) P[x + 1] = P[x] + (double)src[((size_t)y * W + x) * D + d];
+                for (int x = 0; x < W; x++) {
+                    int a[4];
+                    cbca_support(ref, oth, W, y, x, d, side, a);
+                    dst[((size_t)y * W + x) * D + d] = (float)(P[x + a[1] + 1] - P[x - a[0]]);
+                }
             }
-        }
-    free(P);
+        free(P);
+    }
 }
 
 EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
                             int D, int side)
 {
+#pragma omp parallel num_threads(g_threads)
+    {
     double *Q = (double *)malloc(sizeof(double) * (size_t)(H + 1));
     long *N = (long *)malloc(sizeof(long) * (size_t)(H + 1));
+#pragma omp for schedule(static)
     for (int x = 0; x < W; x++)
         for (int d = 0; d < D; d++) {
             Q[0] = 0.0;
@@ -551,6 +651,7 @@ EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, c
         }
     free(Q);
     free(N);
+    }
 }
 
 /* iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv); result in cv. */

@@ -229,6 +229,19 @@ static void cbca_iters(const CbcaVolumes &fwd, const CbcaVolumes &bwd, int nvol,
     }
 }
 
+// The scans address with 32-bit buffer offsets (signed soffsets): the H pass reaches 4*W*D bytes
+// into a row and the V pass (q - qb) <= 3R + 17 rows of 4*W*D bytes past its rebase row (loads
+// prefetched PF = 16 positions ahead of a 2R+2 block that starts R rows after qb); the V pass's
+// arm loads reach 4*H*W bytes.  Beyond that an offset would wrap silently (the column
+// descriptors carry no range limit), so such shapes are refused.
+static bool cbca_shape_ok(int H, int W, int D, int L1)
+{
+    if (H > 65535 || W > 65535) return false;            // grid.y = lines
+    const int R = L1 <= 16 ? 15 : 31;
+    const int64_t row = 4 * (int64_t)W * D;
+    return (3 * R + 18) * row < ((int64_t)1 << 31) && 4 * (int64_t)H * W < ((int64_t)1 << 31);
+}
+
 // fwd: horizontal pass cv -> tmp; bwd: vertical pass tmp -> cv
 static int cbca_launch(float *const cv[2], float *const tmp[2], const uint32_t *const ref[2],
                        const uint32_t *const oth[2], const int side[2], int nvol, int H, int W, int D, int L1,
@@ -265,7 +278,7 @@ SDE_EXPORT int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const u
     if (!cv || !tmp || !arms_ref || !arms_other || H <= 0 || W <= 0 || D <= 0 || iters < 0 || L1 < 1 ||
         L1 > SDE_CBCA_MAX_L1 || (side != SDE_SIDE_LEFT && side != SDE_SIDE_RIGHT) || cv == tmp)
         return SDE_ERR_ARG;
-    if (H > 65535 || W > 65535) return SDE_ERR_ARG;      // grid.y = lines
+    if (!cbca_shape_ok(H, W, D, L1)) return SDE_ERR_ARG;
     float *const cvs[2] = {cv, nullptr}, *const tmps[2] = {tmp, nullptr};
     const uint32_t *const refs[2] = {arms_ref, nullptr}, *const oths[2] = {arms_other, nullptr};
     const int sides[2] = {side, side};
@@ -283,7 +296,7 @@ SDE_EXPORT int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_
     for (int i = 0; i < 4; i++)
         for (int j = i + 1; j < 4; j++)
             if (b[i] == b[j]) return SDE_ERR_ARG;
-    if (H > 65535 || W > 65535) return SDE_ERR_ARG;
+    if (!cbca_shape_ok(H, W, D, L1)) return SDE_ERR_ARG;
     float *const cvs[2] = {cv_l, cv_r}, *const tmps[2] = {tmp_l, tmp_r};
     const uint32_t *const refs[2] = {arms_l, arms_r}, *const oths[2] = {arms_r, arms_l};
     const int sides[2] = {SDE_SIDE_LEFT, SDE_SIDE_RIGHT};

@@ -745,11 +745,13 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
                                                                        nullptr, nullptr, nullptr);
         } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
             // one row sweep per (row, 64-disparity chunk) writes both volumes
-            static const bool attr = [] {
-                return hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess;
-            }();
-            if (!attr) return SDE_ERR_LAUNCH;
+            static std::atomic<uint64_t> attr{0};
+            bool ok = true;
+            once_per_device(attr, [&ok] {
+                ok = hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess;
+            });
+            if (!ok) return SDE_ERR_LAUNCH;
             const int nchunks = cdiv(D, CV_DC);
             cvlr_row_kernel<<<dim3((unsigned)(nchunks * H)), 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
                                                                          out_left, out_right);

@@ -326,14 +326,13 @@ void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int
 {
     int tlo0 = 0, ntw = 0;
     row_window(d0, d1, tlo0, ntw);
-    static bool attr = false;
-    if (!attr) {
+    static std::atomic<uint64_t> attr{0};
+    once_per_device(attr, [] {
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
-        attr = true;
-    }
+    });
     if (out_min)
         cv_wta_row_kernel<true><<<H, 512, row_smem(ntw), st>>>(fl, fr, H, W, d0, d1, tlo0, ntw, out_min, out_arg,
                                                                out_disp, counter, list);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "sde.h"
 
 #define SDE_EXPORT extern "C" __attribute__((visibility("default")))
@@ -19,6 +21,23 @@ static inline int launch_status()
 }
 
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Per-device one-time setup (kernel attributes such as the >64 KB dynamic-LDS opt-in are per
+// device): `done` holds one bit per device id; the first caller on a device runs `fn` and
+// publishes the bit.  Concurrent first calls may both run `fn`, which is idempotent.
+template <typename F>
+static inline void once_per_device(std::atomic<uint64_t> &done, F fn)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        fn();
+        return;
+    }
+    const uint64_t bit = 1ull << dev;
+    if (done.load(std::memory_order_acquire) & bit) return;
+    fn();
+    done.fetch_or(bit, std::memory_order_acq_rel);
+}
 
 // 64-float (256 B) rows in LDS, XOR-swizzled at 16-B granularity: the 16 lanes
 // of one ds_read_b128 group that read the same logical chunk of 16 consecutive

@@ -352,6 +352,11 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             ahead.advance(g);
         }
         if (WTA) {
+            // the lanes read each other's LDS slots: make the cross-lane dependency explicit (one
+            // wave per workgroup, so a wave barrier orders the writes above before these reads)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // PF pixels x 64 lane partials: lane l merges lanes 8(l&7)..+7 of step l>>3 (increasing
             // d), then the 8 octants of its step by xor-butterfly; the merge is a total order
             // (first-min with index tie-break, no NaN partials), so any merge order agrees
@@ -365,6 +370,10 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             for (int o2 = 1; o2 < G; o2 <<= 1) wta_merge(bv, ba, __shfl_xor(bv, o2, 64), __shfl_xor(ba, o2, 64));
             const int px = wpx[st];
             if (q == 0 && px >= 0) sd.disp[px] = (float)(ba == 0x7fffffff ? 0 : ba);
+            // ... and these reads before the next block's writes to the same slots
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
     if (WTA && g.n < nlen) {
@@ -605,7 +614,8 @@ __global__ __launch_bounds__(64) void lrc_cols_kernel(const uint8_t *__restrict_
 __global__ __launch_bounds__(64) void lrc_rows_kernel(const float *__restrict__ dl, const uint8_t *__restrict__ f,
                                                       int H, int W, float *__restrict__ out)
 {
-    __shared__ int16_t sleft[4096];                // nearest unflagged column left of x (-1 = none)
+    // nearest unflagged column left of x (LRC_NONE = none): 2 B per column of the row, W <= 65535
+    extern __shared__ uint16_t sleft[];
     const int y = blockIdx.x;
     const int lane = threadIdx.x;
     const size_t row = (size_t)y * W;
@@ -619,7 +629,8 @@ __global__ __launch_bounds__(64) void lrc_rows_kernel(const float *__restrict__ 
         const int v = wave_max_scan(clear ? x : -1);
         int prev = __shfl_up(v, 1, 64);
         if (lane == 0) prev = -1;
-        if (in) sleft[x] = (int16_t)(prev > carry ? prev : carry);
+        const int lft = prev > carry ? prev : carry;
+        if (in) sleft[x] = lft < 0 ? (uint16_t)LRC_NONE : (uint16_t)lft;
         const int last = __builtin_amdgcn_readlane(v, 63);
         carry = last > carry ? last : carry;
     }
@@ -642,7 +653,7 @@ __global__ __launch_bounds__(64) void lrc_rows_kernel(const float *__restrict__ 
         }
         const uint32_t pk = park[row + x];
         const uint32_t up = pk & 0xFFFFu, down = pk >> 16;
-        const int left = sleft[x];
+        const int left = sleft[x] == LRC_NONE ? -1 : (int)sleft[x];
         int number = 0;
         double sum = 0.0;
         if (up != LRC_NONE) { number++; sum += dl[(size_t)up * W + x]; }
@@ -754,10 +765,19 @@ SDE_EXPORT int sde_lr_check(const float *disp_l, const float *disp_r, int H, int
 SDE_EXPORT int sde_lrc_fill(const float *disp_l, const uint8_t *lrc_l, int H, int W, float *out, void *stream)
 {
     if (!disp_l || !lrc_l || !out || H <= 0 || W <= 0) return SDE_ERR_ARG;
-    if (H >= (int)LRC_NONE || W > 4096 || out == disp_l) return SDE_ERR_ARG;   // 16-bit rows, LDS row
+    // 16-bit row / column indices (0xFFFF = none); the row pass keeps 2 B per column in LDS (<= 128 KB)
+    if (H >= (int)LRC_NONE || W >= (int)LRC_NONE || out == disp_l) return SDE_ERR_ARG;
     hipStream_t st = as_stream(stream);
+    const size_t smem = 2 * (size_t)W;
+    if (smem > 64 * 1024) {
+        static std::atomic<uint64_t> attr{0};
+        once_per_device(attr, [] {
+            (void)hipFuncSetAttribute((const void *)lrc_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      2 * (int)LRC_NONE);
+        });
+    }
     lrc_cols_kernel<<<W, 64, 0, st>>>(lrc_l, H, W, reinterpret_cast<uint32_t *>(out));
-    lrc_rows_kernel<<<H, 64, 0, st>>>(disp_l, lrc_l, H, W, out);
+    lrc_rows_kernel<<<H, 64, smem, st>>>(disp_l, lrc_l, H, W, out);
     return launch_status();
 }
 

@@ -1213,8 +1213,8 @@ SDE_EXPORT int64_t sde_tower_workspace_bytes(int H, int W, int nlayers, int nf)
 
 static void set_tower_attrs()
 {
-    static bool done = false;
-    if (done) return;
+    static std::atomic<uint64_t> done{0};
+    once_per_device(done, [] {
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
     (void)hipFuncSetAttribute((const void *)conv64_mfma_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, TW_SMEM);
@@ -1233,7 +1233,7 @@ static void set_tower_attrs()
     SDE_X6P_ATTR(false, true, false, false);
 #undef SDE_X6P_ATTR1
 #undef SDE_X6P_ATTR
-    done = true;
+    });
 }
 
 static int cu_count()

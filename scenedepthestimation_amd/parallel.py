@@ -80,8 +80,19 @@ def gather_row_bands(band: torch.Tensor, full: torch.Tensor, world: int, group=N
     return full
 
 
+def allreduce_max_(words: torch.Tensor, group=None):
+    """In-place MAX all-reduce of the f16x3 bound words (non-negative floats)."""
+    dist.all_reduce(words, op=dist.ReduceOp.MAX, group=group)
+    return words
+
+
 class DisparityShardedMatcher:
-    """Config 5: features from row bands + all-gather, disparity-sharded fused CV/WTA + all-gather merge."""
+    """Config 5: features from row bands + all-gather, disparity-sharded fused CV/WTA + all-gather merge.
+
+    The tower runs on this rank's row band of both images (band_tower); the f16x3 bound words are
+    all-reduced (MAX) after the image bound and after every layer, so each rank scales every layer
+    by the whole image's bound and its band's features are bit-identical to the single-device
+    tower's rows."""
 
     def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="f16x3"):
         from .pipeline import StereoMatcher
@@ -92,20 +103,41 @@ class DisparityShardedMatcher:
                                tower_precision=tower_precision)
         self.r0, self.r1, self.rpb = row_band(H, world, rank)
         dev = self.m.device
+        L = nlayers
         self.band = torch.zeros((2, self.rpb, W, nf), dtype=torch.float32, device=dev)
+        hb = self.r1 - self.r0
+        # the band's padded rows [r0, r1 + 2L) of both images, contiguous (one batched launch per layer)
+        self.band_pad = torch.empty((2, hb + 2 * L, W + 2 * L), dtype=torch.float32, device=dev) if hb > 0 else None
+        # a short last band writes a contiguous [2, hb, W, nf] buffer first
+        self.band_out = self.band if hb == self.rpb else \
+            (torch.empty((2, hb, W, nf), dtype=torch.float32, device=dev) if hb > 0 else None)
         self.full = torch.empty((world * 2, self.rpb, W, nf), dtype=torch.float32, device=dev)
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
+
+    def band_steps(self):
+        """tower_steps over this rank's band (generator; see pipeline.tower_steps)."""
+        from .pipeline import tower_steps
+        m, L = self.m, self.m.nlayers
+        if self.band_pad is None:
+            return iter(())
+        self.band_pad.copy_(m.img_pad2[:, self.r0:self.r1 + 2 * L])
+        return tower_steps(self.band_pad, m.packed, L, self.band_out, m.ws, m.tower_precision, m.nf)
 
     def features(self):
         from . import ops
         m, L = self.m, self.m.nlayers
-        for i in range(2):
-            ops.preprocess_u8(m.img_u8[i], L, out=m.img_pad[i], stats=m.stats[i])
-            if self.r1 > self.r0:
-                # padded rows [r0, r1 + 2L) produce feature rows [r0, r1)
-                sub = m.img_pad[i][self.r0:self.r1 + 2 * L]
-                ops.tower_forward(sub, m.packed, L, m.nf, out=self.band[i, :self.r1 - self.r0], workspace=m.ws,
-                                  precision=m.tower_precision)
+        ops.preprocess_u8_batch(m.img_u82, L, out=m.img_pad2, stats=m.stats2)
+        if self.band_pad is not None:
+            for _stage, words in self.band_steps():
+                if m.tower_precision == "f16x3":
+                    allreduce_max_(words, self.group)
+            if self.band_out is not self.band:
+                self.band[:, :self.r1 - self.r0].copy_(self.band_out)
+        elif m.tower_precision == "f16x3":
+            # an empty band still joins every bound all-reduce (same count as the other ranks)
+            words = torch.zeros((2, 64), dtype=torch.float32, device=m.device)
+            for _ in range(L - 1):
+                allreduce_max_(words, self.group)
         dist.all_gather_into_tensor(self.full, self.band, group=self.group)
         full = self.full.view(self.world, 2, self.rpb, self.W, m.nf)
         for i in range(2):

@@ -22,6 +22,69 @@ import torch
 from . import mc_cnn, ops
 
 
+AMAX_WORDS = 64   # f16x3 bound words per image in the tower workspace (TOWER_AMAX_BYTES / 4)
+
+
+def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3", nf: int = 64, on_launch=None):
+    """sde_tower_forward_batch's launch sequence (mc_cnn_brunch.py:31-48), one layer at a time, as a
+    generator: the same workspace layout, bound-word memset, image absmax and per-layer launches,
+    so the features are bit-identical to ops.tower_forward_batch.  It yields (stage, words) after the
+    image bound (stage 1) and after every layer l < nlayers (stage l): the points at which a caller
+    may combine the f16x3 bound words of row bands (all-reduce MAX, parallel.py) before the next
+    layer reads them.  on_launch(layer, launch): optional wrapper around each layer's launch (timing).
+
+    img_pad f32 [N, H+2L, W+2L] (contiguous), out f32 [N, H, W, nf], ws uint8 of
+    ops.tower_batch_workspace_bytes(H, W, N, nlayers) bytes (or more)."""
+    L = nlayers
+    N, Hp, Wp = img_pad.shape
+    H, W = Hp - 2 * L, Wp - 2 * L
+    need = ops.tower_batch_workspace_bytes(H, W, N, L, nf)
+    if ws.numel() < need:
+        raise ValueError("tower workspace too small")
+    cbl = precision in ("bf16x6", "f16x3")
+    h2, w2 = H + 2 * (L - 2), W + 2 * (L - 2)
+    act = h2 * w2 * nf if L > 2 else 0
+    wsf = ws[: 2 * N * act * 4 + N * AMAX_WORDS * 4].view(torch.float32)
+    bufs = [wsf[: N * act], wsf[N * act: 2 * N * act]]
+    words = wsf[2 * N * act:].view(N, AMAX_WORDS)
+    f16 = precision == "f16x3"
+    if f16:
+        words.zero_()
+        ops.absmax_batch(img_pad, words)
+    yield 1, words
+
+    def run(layer, fn):
+        if on_launch is None:
+            fn()
+        else:
+            on_launch(layer, fn)
+
+    hin, win = H + 2 * L - 4, W + 2 * L - 4
+    first = out if L == 2 else bufs[0][: N * hin * win * nf].view(N, hin, win, nf)
+    run(2, lambda: ops.tower_layer_batch(img_pad, packed, L, 2, first, nf=nf, precision=precision,
+                                         out_cblock=cbl and L > 2, in_absmax=words[:, 0:1] if f16 else None,
+                                         out_absmax=words[:, 1:2] if (f16 and L > 2) else None))
+    cur = 0
+    for layer in range(3, L + 1):
+        yield layer - 1, words
+        src = bufs[cur][: N * hin * win * nf].view(N, hin, win, nf)
+        o = out if layer == L else bufs[cur ^ 1][: N * (hin - 2) * (win - 2) * nf].view(N, hin - 2, win - 2, nf)
+        run(layer, lambda: ops.tower_layer_batch(src, packed, L, layer, o, nf=nf, precision=precision,
+                                                 in_cblock=cbl, out_cblock=cbl and layer < L,
+                                                 in_absmax=words[:, layer - 2:layer - 1] if f16 else None,
+                                                 out_absmax=words[:, layer - 1:layer] if (f16 and layer < L) else None))
+        hin, win = hin - 2, win - 2
+        cur ^= 1
+
+
+def run_tower(img_pad, packed, nlayers, out, ws, precision="f16x3", nf=64, combine=None, on_launch=None):
+    """Drive tower_steps to the end; combine(words) is applied at every yield (e.g. an all-reduce)."""
+    for _stage, words in tower_steps(img_pad, packed, nlayers, out, ws, precision, nf, on_launch):
+        if combine is not None:
+            combine(words)
+    return out
+
+
 class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
                  nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "f16x3",
@@ -76,13 +139,20 @@ class StereoMatcher:
             t = src if isinstance(src, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(src, np.uint8))
             dst.copy_(t, non_blocking=False)
 
-    def features(self):
-        """Preprocess + tower for both images (compute_feature, process_functional.py:11-45)."""
+    def features(self, on_launch=None):
+        """Preprocess + tower for both images (compute_feature, process_functional.py:11-45).
+        on_launch(layer, launch): run the tower layer by layer from Python (tower_steps: the same
+        launches, bits and workspace as the one-call path) with each launch wrapped, e.g. timed."""
         ops.preprocess_u8_batch(self.img_u82, self.nlayers, out=self.img_pad2, stats=self.stats2)
-        return self.features_from_padded()
+        return self.features_from_padded(on_launch)
 
-    def features_from_padded(self):
+    def features_from_padded(self, on_launch=None):
         """Tower only, on already-normalised padded images in self.img_pad (the pair per launch)."""
+        if on_launch is not None and not self.split:
+            run_tower(self.img_pad2, self.packed, self.nlayers, self.feat2, self.ws, self.tower_precision, self.nf,
+                      on_launch=on_launch)
+            self.split_valid = False
+            return self.feat[0], self.feat[1]
         if self.split:
             for i in range(2):
                 ops.tower_forward(self.img_pad[i], self.packed, self.nlayers, self.nf, out=self.feat[i],
@@ -125,6 +195,7 @@ class StereoMatcher:
             disp=[torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(2)],
             lrc=[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)],
             disp_a=torch.empty((H, W), dtype=torch.float32, device=dev),
+            disp_b=torch.empty((H, W), dtype=torch.float32, device=dev),
         )
         if self.cbca_iters > 0:
             self.sgm_bufs["arms"] = [torch.empty((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
@@ -192,7 +263,8 @@ class StereoMatcher:
         # the interior of disp_l becomes the median of the LRC-filled map.  The reference's
         # right input d_disparityr_a is never written (:1227); here the right map is filtered
         # from its own WTA output (documented divergence, parity unpinned).
-        disp_r_src = b["disp"][1].clone()
+        disp_r_src = b["disp_b"]
+        disp_r_src.copy_(b["disp"][1])
         ops.median5(b["disp_a"], b["disp"][0])
         ops.median5(disp_r_src, b["disp"][1])
         mark("filter", t)

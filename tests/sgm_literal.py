@@ -11,6 +11,7 @@ import numpy as np
 
 
 def _interation(row, col, P1, P2, old, min_cost, min_cost_P2, is_copy, is_first, is_cal_min, cv, S):
+    """min_cost / min_cost_P2: one value per lane (the reference's registers are per thread)."""
     nl = cv.shape[2] // 4
     c = [[float(cv[row, col, 4 * l + i]) for i in range(4)] for l in range(nl)]   # c1..c4 per lane
     if not (is_first or is_copy):
@@ -22,16 +23,29 @@ def _interation(row, col, P1, P2, old, min_cost, min_cost_P2, is_copy, is_first,
                 pre = o1
             if l == nl - 1:                              # disp // 4 == last lane
                 nxt = o4
-            c[l][0] += min(min(pre + P1, o1), min(o2 + P1, min_cost_P2)) - min_cost
-            c[l][1] += min(min(o1 + P1, o2), min(o3 + P1, min_cost_P2)) - min_cost
-            c[l][2] += min(min(o2 + P1, o3), min(o4 + P1, min_cost_P2)) - min_cost
-            c[l][3] += min(min(o3 + P1, o4), min(nxt + P1, min_cost_P2)) - min_cost
+            mc, mcp2 = min_cost[l], min_cost_P2[l]
+            c[l][0] += min(min(pre + P1, o1), min(o2 + P1, mcp2)) - mc
+            c[l][1] += min(min(o1 + P1, o2), min(o3 + P1, mcp2)) - mc
+            c[l][2] += min(min(o2 + P1, o3), min(o4 + P1, mcp2)) - mc
+            c[l][3] += min(min(o3 + P1, o4), min(nxt + P1, mcp2)) - mc
     for l in range(nl):
         for i in range(4):
             S[row, col, 4 * l + i] = np.float32(float(S[row, col, 4 * l + i]) + c[l][i])
     if is_cal_min:
-        min_cost = min(min(min(v[0], v[1]), min(v[2], v[3])) for v in c)
-        min_cost_P2 = min_cost + P2
+        # m1 = min(c1, c2); m2 = min(c3, c4); min_cost = min(m1, m2); then
+        # min_cost = min(min_cost, shfl_xor_sync(min_cost, k)) for k = 1, 2, 4, 8, 16 (one 32-lane warp)
+        # (D != 128: the build's generalisation -- lanes padded to a power of two with +inf)
+        nlp = 1
+        while nlp < nl:
+            nlp <<= 1
+        m = [min(min(v[0], v[1]), min(v[2], v[3])) for v in c] + [float("inf")] * (nlp - nl)
+        k = 1
+        while k < nlp:
+            m = [min(m[l], m[l ^ k]) for l in range(nlp)]
+            k <<= 1
+        m = m[:nl]
+        min_cost = m
+        min_cost_P2 = [v + P2 for v in m]
     return c, min_cost, min_cost_P2
 
 
@@ -43,7 +57,7 @@ def _run_line(steps, cv, S):
     """steps: list of (row, col, P1, P2, is_copy, is_first, is_cal_min)."""
     nl = cv.shape[2] // 4
     old = [[1.0] * 4 for _ in range(nl)]
-    mc, mcp2 = 1.0, 1.0
+    mc, mcp2 = [1.0] * nl, [1.0] * nl
     for (r, c, P1, P2, cp, first, calmin) in steps:
         old, mc, mcp2 = _interation(r, c, P1, P2, old, mc, mcp2, cp, first, calmin, cv, S)
 

@@ -108,6 +108,12 @@ def test_argument_validation_without_gpu():
     assert lib.sde_tower_packed_floats(0, 64) == -1
     assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 4, 8, 14, 1, N) == ERR                          # aliased buffers
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 4, 8, 33, 1, N) == ERR                          # L1 > 32
+    # 32-bit scan offsets: (3R + 18) rows of 4*W*D bytes must stay below 2^31 (R = 15 for L1 <= 16)
+    assert lib.sde_cbca(1, 2, 3, 4, 2, 40000, 256, 1, 14, 0, N) == ERR                            # 63 * 41 MB
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 33300, 256, 14, 0, N) == ERR                    # just past
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 19000, 256, 20, 0, N) == ERR                    # R = 31: 111 rows
+    assert lib.sde_lrc_fill(1, 2, 4, 65535, 3, N) == ERR                                          # 16-bit columns
+    assert lib.sde_lrc_fill(1, 2, 65535, 4, 3, N) == ERR                                          # 16-bit rows
 
 
 def test_ops_refuse_cpu_tensors():

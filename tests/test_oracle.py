@@ -3,8 +3,12 @@
 The golden vectors were produced by the reference's own NumPy functions
 (process_functional.py:48-113, see tests/golden/make_golden.py).
 """
+import os
+
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_golden_cost_volume_bit_exact(oracle, golden, golden_cases):
@@ -127,3 +131,12 @@ def test_tower_oracle_vs_torch_fp64(oracle):
     x = x[0].permute(1, 2, 0)
     x = x / torch.sqrt(torch.clamp((x * x).sum(-1, keepdim=True), min=1e-12))
     assert np.abs(out - x.numpy()).max() < 1e-6
+
+
+def test_oracle_asan():
+    """every oracle entry point runs clean under AddressSanitizer + UBSan
+    (oracle/asan_driver.c; 1 and 3 OpenMP threads, edge shapes, non-finite SGM costs)."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "asan driver ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

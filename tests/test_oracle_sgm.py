@@ -23,6 +23,39 @@ def test_sgm_oracle_matches_literal(oracle, H, W, D):
     assert S_or.tobytes() == S_lit.tobytes()
 
 
+@pytest.mark.parametrize("H,W,D", [(5, 6, 8), (4, 9, 16), (6, 5, 128), (3, 7, 4)])
+def test_sgm_oracle_matches_literal_nonfinite(oracle, H, W, D):
+    """NaN / +-inf costs: the binary-min order and the per-lane minima decide where they propagate."""
+    cv, img = _case(H * 7 + W * 3 + D, H, W, D)
+    rng = np.random.default_rng(D)
+    cv[rng.random(cv.shape) < 0.04] = np.nan
+    cv[rng.random(cv.shape) < 0.04] = np.inf
+    cv[rng.random(cv.shape) < 0.02] = -np.inf
+    cv[1, :, :4] = np.nan                     # a whole first lane NaN on one row
+    pen = oracle.sgm_penalties(img)
+    S_lit = sgm_8path_literal(cv, pen)
+    S_or = oracle.sgm_8path(cv, pen)
+    # NaN payloads are not part of the contract: compare with NaNs canonicalised
+    assert np.array_equal(np.isnan(S_or), np.isnan(S_lit))
+    assert np.nan_to_num(S_or, nan=7.0).tobytes() == np.nan_to_num(S_lit, nan=7.0).tobytes()
+    # the per-lane minima matter: some lane saw a NaN the others ignored
+    assert np.isnan(S_or).any() and np.isfinite(S_or).any()
+
+
+def test_sgm_oracle_threads_bit_identical(oracle):
+    cv, img = _case(11, 30, 41, 64)
+    pen = oracle.sgm_penalties(img)
+    n = oracle.get_threads()
+    try:
+        oracle.set_threads(1)
+        a = oracle.sgm_8path(cv, pen)
+        oracle.set_threads(4)
+        b = oracle.sgm_8path(cv, pen)
+    finally:
+        oracle.set_threads(n)
+    assert a.tobytes() == b.tobytes()
+
+
 def test_sgm_wraps_diagonals(oracle):
     """Wide-short and tall-narrow images: diagonal paths wrap and restart (:570-572, :702-704)."""
     for (H, W) in [(9, 3), (3, 9)]:
