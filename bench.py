@@ -113,55 +113,9 @@ TOWER_ARITH = {
 
 
 def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: Timer):
-    """One pass of the hot path, launched layer by layer so single kernels can be timed."""
-    L = m.nlayers
-    H, W = m.H, m.W
-    # activation ping-pong buffers for layers 3..L, both images (layer 2 output is (H+2(L-2)) x ...)
-    acts = [torch.empty((2 * (H + 2 * (L - 2)) * (W + 2 * (L - 2)) * NF,), dtype=torch.float32, device=m.device)
-            for _ in range(2)]
-    # f16x3 bound words per image (what sde_tower_forward_batch keeps in its workspace)
-    words = torch.zeros((2, L), dtype=torch.float32, device=m.device)
-    batched = m.split is None
-
-    def tower_pair(timed):
-        """Preprocess both images, then the tower layer by layer with both images per launch
-        (sde_tower_layer_batch = what sde_tower_forward_batch launches), layer 3 timed."""
-        e_t = t_tower.start() if timed == "stages" else None
-        ops.preprocess_u8_batch(m.img_u82, L, out=m.img_pad2, stats=m.stats2)
-        if not batched:   # split planes requested: per-image launches
-            m.features_from_padded()
-            if e_t is not None:
-                t_tower.stop(e_t)
-            return
-        # split arithmetics: intermediate activations in the c-block-major layout, as sde_tower_forward runs them
-        cbl = m.tower_precision in ("bf16x6", "f16x3")
-        if m.tower_precision == "f16x3":
-            words.zero_()
-            ops.absmax_batch(m.img_pad2, words)
-        hin, win = H + 2 * L - 4, W + 2 * L - 4
-        first_out = acts[0][: 2 * hin * win * NF].view(2, hin, win, NF) if L > 2 else m.feat2
-        ops.tower_layer_batch(m.img_pad2, m.packed, L, 2, first_out, precision=m.tower_precision,
-                              out_cblock=cbl and L > 2, in_absmax=words[:, 0:1],
-                              out_absmax=words[:, 1:2] if L > 2 else None)
-        cur = 0
-        for layer in range(3, L + 1):
-            if layer == L:
-                o = m.feat2
-            else:   # a contiguous prefix of the ping-pong buffer, viewed at this layer's size
-                o = acts[cur ^ 1][: 2 * (hin - 2) * (win - 2) * NF].view(2, hin - 2, win - 2, NF)
-            src = acts[cur][: 2 * hin * win * NF].view(2, hin, win, NF)
-            e = t_conv.start() if (timed == "conv" and layer == 3) else None
-            ops.tower_layer_batch(src, m.packed, L, layer, o, precision=m.tower_precision,
-                                  in_cblock=cbl, out_cblock=cbl and layer < L, in_absmax=words[:, layer - 2:layer - 1],
-                                  out_absmax=words[:, layer - 1:layer] if layer < L else None)
-            if e is not None:
-                t_conv.stop(e)
-            hin, win = hin - 2, win - 2
-            cur ^= 1
-        if e_t is not None:
-            t_tower.stop(e_t)
-        m.split_valid = False
-
+    """One pass of the hot path.  The tower runs through the shipped StereoMatcher.features with a
+    launch hook (pipeline.tower_steps: the same launches and bits as the one-call
+    sde_tower_forward_batch, checked in main), so single kernels can be timed."""
     if what == "tower+cbca+sgm":
         def step_sgm(timed=None):
             e = t_tower.start() if timed == "stages" else None
@@ -175,11 +129,20 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
             return out
         return step_sgm
 
+    def conv_hook(layer, launch):
+        e = t_conv.start() if layer == 3 else None
+        launch()
+        if e is not None:
+            t_conv.stop(e)
+
     def step(timed=None):
         """timed: None (warm-up), "conv" (the timed region: HIP events around the roofline kernel
         only) or "stages" (after the timed region: events around the tower and the CV+WTA)."""
         if what == "tower+cv_wta":
-            tower_pair(timed)
+            e_t = t_tower.start() if timed == "stages" else None
+            m.features(on_launch=conv_hook if timed == "conv" else (lambda layer, launch: launch()))
+            if e_t is not None:
+                t_tower.stop(e_t)
         e = t_cv.start() if timed == "stages" else None
         m.cost_wta()
         if e is not None:
@@ -190,10 +153,14 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
 
 
 def cpu_baseline(H, W, D, what, budget_s=15.0):
-    """The C oracle (single thread, exact) on a bounded row band of the same workload."""
+    """The C oracle (exact) on a bounded sample of the same workload: one thread, then the host's CPU
+    share (min(16, cpu_count): row bands on Python threads for the tower + CV/WTA path, OpenMP over
+    scanlines for the SGM path)."""
     import oracle
     from scenedepthestimation_amd import mc_cnn
     oracle.build()
+    oracle.set_threads(1)
+    nt = min(16, os.cpu_count() or 1)
     left, right, _ = stereo_pair(H, W, D, seed=0)
     w = mc_cnn.synthetic_weights(NLAYERS)
     hw, hb = mc_cnn.layer_lists(w, NLAYERS)
@@ -234,14 +201,16 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
             a, _ = oracle.lr_check(dl, dr)
             oracle.median5(oracle.lrc_fill(dl, a), dl)
             return time.perf_counter() - t0
+        oracle.set_threads(nt)
         hc, wc = 16, max(D + 16, 64)
         t1 = run_crop(hc, wc)
         hc = int(max(16, min(H, hc * budget_s / max(t1, 1e-6))))
         t = run_crop(hc, wc)
-        return {"value": hc * wc * D / t / 1e6, "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
+        oracle.set_threads(1)
+        return {"value": hc * wc * D / t / 1e6, "unit": "Mpixel-disparities/s", "cores": nt, "kind": "port",
                 "sample": f"{hc} x {wc} crop x D={D} of the {H}x{W} pair through the full GPU path restated in C "
                           f"(fp64 tower, L/R cost volume, CBCA x{CBCA_ITERS}, 8-path SGM both sides, WTA, LR check, "
-                          f"LRC, median), {t:.1f} s"}
+                          f"LRC, median), OpenMP over scanlines on {nt} threads, {t:.1f} s"}
     t1 = run(1)
     rows = int(max(1, min(H, budget_s / max(t1, 1e-6))))
     t = run(rows)
@@ -249,7 +218,6 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
     desc = (f"({what}, exact C restatement, {'fp64 tower + ' if what == 'tower+cv_wta' else ''}pairwise-f32 cost "
             f"+ WTA1)")
     # the same restatement on the host's CPU share (ctypes releases the GIL: one row band per thread)
-    nt = min(16, os.cpu_count() or 1)
     if what == "tower+cv_wta" and nt > 1:
         import concurrent.futures as cf
         rows_mt = int(min(H, rows * nt))
@@ -271,6 +239,71 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
                 "single_thread": {"value": single, "cores": 1, "sample": f"{rows} rows, {t:.1f} s"}}
     return {"value": single, "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
             "sample": f"{rows} of {H} rows x {W} cols x D={D} {desc}, {t:.1f} s"}
+
+
+def _events_ms(fn, reps=3):
+    """Mean HIP-event time of fn() on torch's current stream over `reps` calls (after one warm call)."""
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
+    """The reference's GPU path (disparity_compute_by_gpu, process_functional.py:1093-1267, + the
+    build-defined CBCA) on m's resident features: whole-path time and the HBM fraction of each
+    cost-volume / aggregation kernel on SURVEY.md sec. 8(d)'s algorithmic bytes (north_star's
+    "cost-volume + aggregation kernels"), each launch timed alone with HIP events."""
+    H, W, D = m.H, m.W, m.D
+    vox = float(H) * W * D
+    b = m.sgm_bufs
+    out = {}
+    path_ms = _events_ms(lambda: m.sgm_path(post=True))
+    tower_ms = _events_ms(lambda: m.features())
+    out[prefix + "gpu_path_ms"] = path_ms
+    out[prefix + "ms_per_pair_tower_plus_gpu_path"] = tower_ms + path_ms
+    kern = {}
+    # cvlr_row_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes
+    ms = _events_ms(lambda: ops.cost_volume(m.feat[0], m.feat[1], D, layout="HWD", right=True, invalid=1.0,
+                                            out_left=b["cv"][0], out_right=b["cv"][1]))
+    kern["cvlr_row_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
+    if m.cbca_iters > 0:
+        # one CBCA iteration of both sides: H and V pass read + write 4 B/voxel each
+        ms = _events_ms(lambda: ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], m.cbca_L1, 1,
+                                              tmp_l=b["S"][0], tmp_r=b["S"][1]))
+        kern["cbca_scan_kernel (1 iteration, both sides)"] = (ms, 2 * 16.0 * vox)
+    ms = _events_ms(lambda: ops.sgm_8path_wta_pair(b["cv"][0], b["pen"][0], b["S"][0], b["disp"][0], b["cv"][1],
+                                                   b["pen"][1], b["S"][1], b["disp"][1], zero_du_penalties=True))
+    # per side: UD+DU 8 B/voxel, five passes 12 B, DU-RL + WTA 8 B, + 4 B/pixel of disparity
+    kern["sgm_scan_kernel (8 paths + WTA, both sides, 7 launches)"] = (ms, 2 * (76.0 * vox + 4.0 * H * W))
+    per = {}
+    tb = tt = 0.0
+    for k, (ms, byt) in kern.items():
+        gbs = byt / (ms * 1e-3) / 1e9
+        per[k] = {"ms": ms, "GB": byt / 1e9, "GB_s": gbs, "hbm_frac": gbs / PEAK_HBM_GBS}
+        n = m.cbca_iters if k.startswith("cbca") else 1
+        tb += byt * n
+        tt += ms * n
+    out[prefix + "cv_aggregation_kernels"] = per
+    out[prefix + "cv_aggregation_aggregate"] = {
+        "ms": tt, "GB": tb / 1e9, "GB_s": tb / (tt * 1e-3) / 1e9, "hbm_frac": tb / (tt * 1e-3) / 1e9 / PEAK_HBM_GBS,
+        "what": f"cvlr + {m.cbca_iters} x CBCA pair iteration + SGM pair on sec. 8(d) algorithmic bytes"}
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def main():
@@ -343,6 +376,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
 
     roof = None
+    parity = None
     stages = {}
     if what == "tower+cbca+sgm" and (args.mode == "pairdp" or world == 1):
         stages["tower_ms_pair"] = t_tower.mean_ms()
@@ -350,29 +384,15 @@ def main():
         tim = {}
         m.sgm_path(post=True, timings=tim)           # one synchronised pass, per-stage wall times
         stages.update({f"{k}_ms": v * 1e3 for k, v in tim.items()})
-        b = m.sgm_bufs
-        # the SGM pair (both sides, 8 directions = 8 launches) timed alone with HIP events
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        ops.sgm_8path_wta_pair(b["cv"][0], b["pen"][0], b["S"][0], b["disp"][0], b["cv"][1], b["pen"][1],
-                               b["S"][1], b["disp"][1], zero_du_penalties=True)
-        e1.record()
-        torch.cuda.synchronize()
-        sgm_ms = e0.elapsed_time(e1)
-        # per side: UD+DU pass reads C, writes S (8 B/voxel); 5 passes read C, S and write S (12 B);
-        # the last pass (WTA fused) reads C, S (8 B) and writes 4 B per pixel
-        sgm_bytes = 2 * (76.0 * vox + 4.0 * H * W)
-        # one CBCA iteration of both sides (sde_cbca_pair: 2 launches; S buffers as scratch, as in sgm_path)
-        e0.record()
-        ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], CBCA_L1, 1, tmp_l=b["S"][0],
-                      tmp_r=b["S"][1])
-        e1.record()
-        torch.cuda.synchronize()
-        cb_ms = e0.elapsed_time(e1)
-        stages["cbca_pair_iter_ms"] = cb_ms
-        # 2 sides x 2 passes x (read + write) x 4 B
-        stages["cbca_pair_iter_hbm_GBs"] = 2 * 16.0 * vox / (cb_ms * 1e-3) / 1e9
+        g = gpu_path_stages(m)
+        stages.update(g)
+        sgm_ms, sgm_bytes = None, 2 * (76.0 * vox + 4.0 * H * W)
+        for k, v in g["cv_aggregation_kernels"].items():
+            if k.startswith("sgm"):
+                sgm_ms = v["ms"]
+            if k.startswith("cbca"):
+                stages["cbca_pair_iter_ms"] = v["ms"]
+                stages["cbca_pair_iter_hbm_GBs"] = v["GB_s"]
         stages["sgm_pair_ms"] = sgm_ms
         ach = sgm_bytes / (sgm_ms * 1e-3) / 1e9
         roof = {"kernel": "sgm_scan_kernel (8-path SGM + WTA, both sides, 7 launches: DU folded into UD, WTA "
@@ -434,6 +454,34 @@ def main():
                 m.load_images(left, right)
                 m.match().cpu()
             stages["ms_per_pair_host_io"] = (time.perf_counter() - t0) / 5 * 1e3
+            # parity, outside the timed region: (1) the hooked layer-by-layer tower the timed steps ran
+            # == the one-call sde_tower_forward_batch; (2) the certified map == the exact kernel's
+            # over every pixel (and the minimum costs bit for bit)
+            m.features(on_launch=lambda layer, launch: launch())
+            hooked = m.feat2.clone()
+            m.features()
+            same_feat = bool(torch.equal(hooked, m.feat2))
+            cert_disp, cert_min, _ = ops.cv_wta(m.feat[0], m.feat[1], 0, D, want=("disp", "min"), mode="certified",
+                                                workspace=m.cv_ws)
+            ex_disp, ex_min, _ = ops.cv_wta(m.feat[0], m.feat[1], 0, D, want=("disp", "min"), mode="exact")
+            same_disp = bool(torch.equal(cert_disp, ex_disp))
+            same_min = bool(torch.equal(cert_min.view(torch.int32), ex_min.view(torch.int32)))
+            parity = {"checked": True, "pixels": H * W,
+                      "certified_vs_exact_disparity_identical": same_disp,
+                      "certified_vs_exact_min_cost_bits_identical": same_min,
+                      "tower_hooked_vs_one_call_identical": same_feat}
+            if not (same_disp and same_min and same_feat):
+                raise SystemExit(f"parity check failed: {parity}")
+            del cert_disp, cert_min, ex_disp, ex_min, hooked
+            # the reference's default GPU path at the same size (match_single.py:49 ->
+            # disparity_compute_by_gpu), + the build-defined CBCA x2: north_star's own target
+            ms_ = StereoMatcher(H, W, D, tower_precision=args.tower_precision, sgm=True, cbca_iters=CBCA_ITERS,
+                                cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
+            ms_.load_images(left, right)
+            ms_.features()
+            stages["reference_gpu_path"] = gpu_path_stages(ms_)
+            del ms_
+            torch.cuda.empty_cache()
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             kname = ("cv_wta_row_kernel + cv_wta_fixup_kernel (certified fused cost volume + WTA)"
@@ -456,6 +504,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(H, W, D, what)
+        cpu["cpu_model"] = cpu_model()
+        cpu["host_cpus_visible"] = os.cpu_count()
 
     if rank == 0:
         line = {
@@ -470,6 +520,8 @@ def main():
                        "pipeline": what, "global_batch": pairs_per_step, "parallelism": par},
             "roofline": roof, "cpu_baseline": cpu, "stages": stages,
         }
+        if parity is not None:
+            line["parity"] = parity
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -601,24 +601,30 @@ static inline void cbca_support(const uint32_t *ref, const uint32_t *oth, int W,
     }
 }
 
-/* side: 1 = left-referenced volume (other pixel x - d), 2 = right-referenced (x + d). */
+/* side: 1 = left-referenced volume (other pixel x - d), 2 = right-referenced (x + d).
+ * Loops run d innermost (contiguous voxels); every (line, d) prefix is still accumulated
+ * sequentially along its line, so the arithmetic is the definition's. */
 EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
                             int D, int side)
 {
 #pragma omp parallel num_threads(g_threads)
     {
-        double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1));   /* P[x + 1] = prefix through x */
+        /* P[(x + 1) * D + d] = prefix of line (y, d) through x; P[d] = 0 */
+        double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1) * D);
 #pragma omp for schedule(static)
-        for (int y = 0; y < H; y++)
-            for (int d = 0; d < D; d++) {
-                P[0] = 0.0;
-                for (int x = 0; x < W; x++) P[x + 1] = P[x] + (double)src[((size_t)y * W + x) * D + d];
-                for (int x = 0; x < W; x++) {
+        for (int y = 0; y < H; y++) {
+            for (int d = 0; d < D; d++) P[d] = 0.0;
+            for (int x = 0; x < W; x++)
+                for (int d = 0; d < D; d++)
+                    P[(size_t)(x + 1) * D + d] = P[(size_t)x * D + d] + (double)src[((size_t)y * W + x) * D + d];
+            for (int x = 0; x < W; x++)
+                for (int d = 0; d < D; d++) {
                     int a[4];
                     cbca_support(ref, oth, W, y, x, d, side, a);
-                    dst[((size_t)y * W + x) * D + d] = (float)(P[x + a[1] + 1] - P[x - a[0]]);
+                    dst[((size_t)y * W + x) * D + d] =
+                        (float)(P[(size_t)(x + a[1] + 1) * D + d] - P[(size_t)(x - a[0]) * D + d]);
                 }
-            }
+        }
         free(P);
     }
 }
@@ -628,29 +634,35 @@ EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, c
 {
 #pragma omp parallel num_threads(g_threads)
     {
-    double *Q = (double *)malloc(sizeof(double) * (size_t)(H + 1));
-    long *N = (long *)malloc(sizeof(long) * (size_t)(H + 1));
+        /* Q / N[(y + 1) * D + d]: prefix of column (x, d) through row y */
+        double *Q = (double *)malloc(sizeof(double) * (size_t)(H + 1) * D);
+        long *N = (long *)malloc(sizeof(long) * (size_t)(H + 1) * D);
 #pragma omp for schedule(static)
-    for (int x = 0; x < W; x++)
-        for (int d = 0; d < D; d++) {
-            Q[0] = 0.0;
-            N[0] = 0;
-            for (int y = 0; y < H; y++) {
-                int b[4];
-                cbca_support(ref, oth, W, y, x, d, side, b);
-                Q[y + 1] = Q[y] + (double)src[((size_t)y * W + x) * D + d];
-                N[y + 1] = N[y] + b[0] + b[1] + 1;
+        for (int x = 0; x < W; x++) {
+            for (int d = 0; d < D; d++) {
+                Q[d] = 0.0;
+                N[d] = 0;
             }
-            for (int y = 0; y < H; y++) {
-                int a[4];
-                cbca_support(ref, oth, W, y, x, d, side, a);
-                const double num = Q[y + a[3] + 1] - Q[y - a[2]];
-                const long cnt = N[y + a[3] + 1] - N[y - a[2]];
-                dst[((size_t)y * W + x) * D + d] = (float)(num / (double)cnt);
-            }
+            for (int y = 0; y < H; y++)
+                for (int d = 0; d < D; d++) {
+                    int b[4];
+                    cbca_support(ref, oth, W, y, x, d, side, b);
+                    const size_t i = (size_t)(y + 1) * D + d, j = (size_t)y * D + d;
+                    Q[i] = Q[j] + (double)src[((size_t)y * W + x) * D + d];
+                    N[i] = N[j] + b[0] + b[1] + 1;
+                }
+            for (int y = 0; y < H; y++)
+                for (int d = 0; d < D; d++) {
+                    int a[4];
+                    cbca_support(ref, oth, W, y, x, d, side, a);
+                    const size_t hi = (size_t)(y + a[3] + 1) * D + d, lo = (size_t)(y - a[2]) * D + d;
+                    const double num = Q[hi] - Q[lo];
+                    const long cnt = N[hi] - N[lo];
+                    dst[((size_t)y * W + x) * D + d] = (float)(num / (double)cnt);
+                }
         }
-    free(Q);
-    free(N);
+        free(Q);
+        free(N);
     }
 }
 

@@ -1,0 +1,241 @@
+"""GPU parity at the BASELINE.json configurations' own sizes.
+
+C1/C2  Middlebury-2003 'cones' 450x375, D = 64: CLI (match_single --cpu-path) and
+       StereoMatcher vs WTA1(compute_cost_volume) of the same features (oracle),
+       tower vs the fp64 restatement on a row band.
+north  1024x1024, D = 192: certified CV+WTA vs the exact kernel over the full map,
+       a row band vs the oracle.
+C3/C4  Middlebury-2014 2000x3000 and Middlebury-2005/06 1110x1390, D = 256: the whole
+       GPU path (L/R volumes, CBCA x2, penalties, 8-path SGM both sides, WTA, LR check,
+       LRC, median) vs the oracle composition on the same features, bit-exact.
+C5     3840x2160, D = 512: 8 disparity shards run one after another on one GPU and merged
+       vs the unsharded map; a row band vs the oracle; the row-band tower with all-reduced
+       bound words (emulated 8 ranks) vs the full-image tower, bit-identical.
+
+The oracle runs on the host's CPU share with OpenMP (oracle.set_threads).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def oracle_threads(oracle):
+    n = oracle.get_threads()
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    yield
+    oracle.set_threads(n)
+
+
+def _weights(L=5):
+    from scenedepthestimation_amd import mc_cnn
+    return mc_cnn.layer_lists(mc_cnn.synthetic_weights(L), L)
+
+
+# ----------------------------------------------------------------------------
+# C1 / C2: cones 450 x 375, D = 64
+# ----------------------------------------------------------------------------
+def test_config_cones_cli_and_matcher(gpu, oracle, tmp_path, monkeypatch):
+    from scenedepthestimation_amd import imageio, match_single
+    from scenedepthestimation_amd import process_functional as pf
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    H, W, D = 375, 450, 64
+    left, right, _ = stereo_pair(H, W, D, seed=31)
+    imageio.imwrite(str(tmp_path / "eval" / "left_1.png"), left)
+    imageio.imwrite(str(tmp_path / "eval" / "right_1.png"), right)
+    monkeypatch.chdir(tmp_path)
+    match_single.main(["-i", "1", "-g", "0", "--checkpoint", "synthetic", "--cpu-path", "--ndisp", str(D)])
+    cli = imageio.imread_gray(str(tmp_path / "result" / "11_11" / "ld1.png"))
+    # the same features the CLI computed (host z-norm, compute_feature) -> the oracle's CPU path
+    ln = match_single.normalise(left.astype(np.float32))
+    rn = match_single.normalise(right.astype(np.float32))
+    fl, fr = pf.compute_feature(ln, rn, 11, 11, 64, "synthetic")
+    want = oracle.WTA1(oracle.compute_cost_volume(fl, fr, D))
+    assert np.array_equal(cli, want.astype(np.uint8))
+    # device preprocess + tower + certified fused CV/WTA (the north-star path at the cones size)
+    m = StereoMatcher(H, W, D)
+    m.load_images(left, right)
+    disp = host(m.match())
+    gl, gr = host(m.feat[0]), host(m.feat[1])
+    assert np.array_equal(disp, oracle.WTA1(oracle.compute_cost_volume(gl, gr, D)))
+    # tower vs the fp64 restatement on a row band (rows 180..199 of the left image)
+    hw, hb = _weights()
+    pad = host(m.img_pad[0])
+    ref = oracle.tower_forward(pad[180:200 + 10], hw, hb)
+    assert np.abs(gl[180:200] - ref).max() < 1e-5
+
+
+# ----------------------------------------------------------------------------
+# north star: 1024 x 1024, D = 192
+# ----------------------------------------------------------------------------
+def test_north_star_certified_equals_exact_full_map(gpu, oracle):
+    from scenedepthestimation_amd import ops
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    H, W, D = 1024, 1024, 192
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    m = StereoMatcher(H, W, D)
+    m.load_images(left, right)
+    disp = m.match().clone()
+    nfix = ops.cv_wta_fixups(m.cv_ws)
+    exact, emin, earg = ops.cv_wta(m.feat[0], m.feat[1], 0, D, want=("disp", "min", "argmin"), mode="exact")
+    _, cmin, carg = ops.cv_wta(m.feat[0], m.feat[1], 0, D, want=("min", "argmin"), mode="certified")
+    assert torch.equal(disp, exact) and torch.equal(carg, earg)
+    assert host(cmin).tobytes() == host(emin).tobytes()
+    assert 0 < nfix < H * W // 100          # some near-ties resolved exactly, most pixels certified
+    fl, fr = host(m.feat[0][500:508]), host(m.feat[1][500:508])
+    omn, oam = oracle.cv_wta_shard(fl, fr, 0, D)
+    assert np.array_equal(host(earg[500:508]), oam) and host(emin[500:508]).tobytes() == omn.tobytes()
+
+
+# ----------------------------------------------------------------------------
+# C3 / C4: the reference's GPU path (+ CBCA) at full resolution, D = 256
+# ----------------------------------------------------------------------------
+def _progress(msg, t0=[None]):
+    import time
+    t = time.time()
+    if t0[0] is None:
+        t0[0] = t
+    print(f"  [{t - t0[0]:7.1f} s] {msg}", flush=True)   # a long oracle run keeps printing (-s)
+
+
+def _sgm_path_vs_oracle(oracle, H, W, D, seed, cbca_iters=2, L1=14, tau=0.02):
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    left, right, _ = stereo_pair(H, W, D, seed=seed)
+    m = StereoMatcher(H, W, D, sgm=True, cbca_iters=cbca_iters, cbca_L1=L1, cbca_tau=tau)
+    m.load_images(left, right)
+    m.features()
+    dl, dr = m.sgm_path(post=True)
+    dl, dr = host(dl), host(dr)
+    fl, fr = host(m.feat[0]), host(m.feat[1])
+    P = m.nlayers
+    zl = host(m.img_pad[0])[P:P + H, P:P + W]      # the device z-norm the arms are built from
+    zr = host(m.img_pad[1])[P:P + H, P:P + W]
+    del m
+    torch.cuda.empty_cache()
+    _progress(f"GPU path done at {H}x{W}x{D}; oracle cost volumes")
+    cl, cr = oracle.cost_volume_hwd(fl, fr, D, invalid=1.0, right=True)
+    del fl, fr
+    if cbca_iters:
+        _progress("oracle CBCA")
+        al, ar = oracle.cbca_arms(zl, L1, tau), oracle.cbca_arms(zr, L1, tau)
+        cl = oracle.cbca(cl, al, ar, "left", cbca_iters)
+        cr = oracle.cbca(cr, ar, al, "right", cbca_iters)
+    _progress("oracle SGM left")
+    wl = oracle.wta_sgm(oracle.sgm_8path(cl, oracle.sgm_penalties(left)))
+    del cl
+    _progress("oracle SGM right")
+    wr = oracle.wta_sgm(oracle.sgm_8path(cr, oracle.sgm_penalties(right)))
+    del cr
+    _progress("oracle post-processing")
+    a, _ = oracle.lr_check(wl, wr)
+    assert np.array_equal(dl, oracle.median5(oracle.lrc_fill(wl, a), wl))
+    assert np.array_equal(dr, oracle.median5(wr, wr))
+    return dl
+
+
+@pytest.mark.timeout(900)
+def test_config4_middlebury0506_sgm_path_bit_exact(gpu, oracle):
+    d = _sgm_path_vs_oracle(oracle, 1110, 1390, 256, seed=4)
+    assert len(np.unique(d)) > 20
+
+
+@pytest.mark.timeout(900)
+def test_config3_middlebury2014_sgm_path_bit_exact(gpu, oracle):
+    d = _sgm_path_vs_oracle(oracle, 2000, 3000, 256, seed=3)
+    assert len(np.unique(d)) > 20
+
+
+# ----------------------------------------------------------------------------
+# C5: 4K, D = 512, 8 disparity shards
+# ----------------------------------------------------------------------------
+def _band_features(m, world, precision):
+    """The row-band tower of `world` emulated ranks (parallel.DisparityShardedMatcher's schedule),
+    their bound words combined by MAX at every step, assembled into full feature maps."""
+    from scenedepthestimation_amd import ops
+    from scenedepthestimation_amd.parallel import row_band
+    from scenedepthestimation_amd.pipeline import tower_steps
+    L, H, W = m.nlayers, m.H, m.W
+    gens, outs = [], []
+    for r in range(world):
+        r0, r1, _ = row_band(H, world, r)
+        if r1 <= r0:
+            continue
+        band_pad = m.img_pad2[:, r0:r1 + 2 * L].contiguous()
+        out = torch.empty((2, r1 - r0, W, 64), dtype=torch.float32, device=m.device)
+        ws = torch.empty(ops.tower_batch_workspace_bytes(r1 - r0, W, 2, L), dtype=torch.uint8, device=m.device)
+        gens.append(tower_steps(band_pad, m.packed, L, out, ws, precision))
+        outs.append((r0, r1, out, ws, band_pad))
+    while True:
+        steps = [next(g, None) for g in gens]
+        if steps[0] is None:
+            assert all(s is None for s in steps)
+            break
+        words = [s[1] for s in steps]
+        mx = torch.stack(words).amax(0)
+        for w in words:
+            w.copy_(mx)
+    full = torch.empty((2, H, W, 64), dtype=torch.float32, device=m.device)
+    for r0, r1, out, _, _ in outs:
+        full[:, r0:r1] = out
+    return full
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x6", "fp32"])
+@pytest.mark.parametrize("H,W,world", [(150, 300, 3), (97, 64, 8), (40, 70, 2)])
+def test_row_band_tower_bit_identical(gpu, precision, H, W, world):
+    """Config 5's sharded tower: bands with all-reduced bound words == the full-image tower."""
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    left, right, _ = stereo_pair(H, W, 32, seed=H)
+    m = StereoMatcher(H, W, 32, tower_precision=precision)
+    m.load_images(left, right)
+    m.features()
+    full = _band_features(m, world, precision)
+    assert torch.equal(full, m.feat2)
+
+
+@pytest.mark.timeout(900)
+def test_config5_4k_d512_shards_and_band_tower(gpu, oracle):
+    from scenedepthestimation_amd import ops
+    from scenedepthestimation_amd.parallel import shard_range
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    H, W, D, N = 2160, 3840, 512, 8
+    left, right, _ = stereo_pair(H, W, D, seed=5)
+    m = StereoMatcher(H, W, D)
+    m.load_images(left, right)
+    m.features()
+    ref_disp = m.cost_wta().clone()
+    # the sharded tower: 8 row bands with all-reduced (emulated) bound words
+    assert torch.equal(_band_features(m, N, "f16x3"), m.feat2)
+    torch.cuda.empty_cache()
+    mins = torch.empty((N, H, W), dtype=torch.float32, device="cuda")
+    args = torch.empty((N, H, W), dtype=torch.int32, device="cuda")
+    for s in range(N):
+        d0, d1 = shard_range(D, N, s)
+        ops.cv_wta(m.feat[0], m.feat[1], d0, d1, min_cost=mins[s], argmin=args[s], want=(), workspace=m.cv_ws)
+    merged = ops.argmin_merge(mins, args)
+    assert torch.equal(merged, ref_disp)
+    rows = slice(1000, 1016)
+    fl, fr = host(m.feat[0][rows]), host(m.feat[1][rows])
+    _, oam = oracle.cv_wta_shard(fl, fr, 0, D)
+    assert np.array_equal(host(ref_disp[rows]), oam.astype(np.float32))
