@@ -332,6 +332,10 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
                 if (xr >= 0 && xr < W) outr[(rowvox + xr) * D + dc + lane] = rring[cvr_rword(xr, lane)];
             }
         }
+        // the next strip's [A] stages its own pixels into the R-ring half these rows occupy:
+        // every wave must be done emitting first (without this barrier a fast wave overwrote a
+        // 64-disparity run a slow wave had not emitted yet -- rare, timing dependent)
+        __syncthreads();
     }
 }
 
