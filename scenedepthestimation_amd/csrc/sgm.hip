@@ -95,6 +95,150 @@ __device__ __forceinline__ double wave_min_f64(double v)
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
+// ---------------------------------------------------------------------------
+// Non-finite costs.  The fast recurrence above (min chain in any order, one wave-wide minimum)
+// equals the reference's for finite costs: its minima are then plain minima.  With NaN / inf in
+// the costs the reference's exact arithmetic decides where they propagate (SGM_Interation,
+// process_functional.py:265-343): Numba's binary min(a, b) = b if b < a else a (a NaN first
+// argument sticks, a NaN second one is ignored), the chain
+//   c += min(min(L(d-1) + P1, L(d)), min(L(d+1) + P1, mcP2)) - mc
+// with L(d-1) := L(d) at d = 0 and L(d+1) := L(d) at d = D-1, and the minimum kept PER
+// reference lane of 4 disparities: min(min(c1, c2), min(c3, c4)), then an xor butterfly
+// min(m, shfl_xor(m, k)), k = 1, 2, 4, .. -- with NaN present lanes can end with different
+// minima, and each uses its own at the next step.  A line switches to this "faithful" step
+// (sticky) at the first step whose costs are not all finite: every earlier state is finite, so
+// it carries over exactly.  Generic D (the reference has D = 128 only): lanes of 4, missing
+// disparities of the last lane and padding lanes up to a power of two act as +inf.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double pymin(double a, double b) { return b < a ? b : a; }
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int DPL>
+__device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL])
+{
+    bool nf = false;
+#pragma unroll
+    for (int i = 0; i < DPL; i++) nf |= __builtin_amdgcn_classf(c[i], 0x207);   // s/qNaN, -inf, +inf
+    return __builtin_amdgcn_ballot_w64(nf) != 0;
+}
+
+// LDS of the faithful step (wave-private): the step's path costs, then one minimum per reference lane
+template <int DPL>
+struct FaithLds {
+    double L[64 * DPL];
+    double v[128];
+};
+
+// One SGM_Interation in the reference's exact arithmetic (see above).  mv / mpv: this lane's
+// disparities' reference-lane minimum and minimum + P2 from the previous step; updated here.
+template <int DPL>
+__device__ __forceinline__ void faithful_step(double (&Ln)[DPL], const double (&L)[DPL], const float (&c)[DPL],
+                                           bool restart, double p1, double p2, double (&mv)[DPL],
+                                           double (&mpv)[DPL], int D, int dbase, FaithLds<DPL> &lds)
+{
+    const int lane = threadIdx.x & 63;
+    if (restart) {
+#pragma unroll
+        for (int i = 0; i < DPL; i++) Ln[i] = (double)c[i];
+    } else {
+        const double lo = dpp_f64<0x138>(L[DPL - 1]);   // wave_shr:1 -> L'(dbase - 1)
+        const double hi = dpp_f64<0x130>(L[0]);         // wave_shl:1 -> L'(dbase + DPL)
+#pragma unroll
+        for (int i = 0; i < DPL; i++) {
+            const int d = dbase + i;
+            const double self = L[i];
+            const double lft = d > 0 ? (i > 0 ? L[i - 1] : lo) : self;
+            const double rgt = d < D - 1 ? (i < DPL - 1 ? L[i + 1] : hi) : self;
+            const double m1 = pymin(lft + p1, self);
+            const double m2 = pymin(rgt + p1, mpv[i]);
+            Ln[i] = (double)c[i] + (pymin(m1, m2) - mv[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < DPL; i++)
+        if (dbase + i < D) lds.L[dbase + i] = Ln[i];
+    wave_sync();
+    const int nl = (D + 3) / 4;
+    int nlp = 1;
+    while (nlp < nl) nlp <<= 1;
+    double v[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int j = lane + 64 * t;
+        double q[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = (j < nl && 4 * j + k < D) ? lds.L[4 * j + k] : __builtin_inf();
+        v[t] = pymin(pymin(q[0], q[1]), pymin(q[2], q[3]));
+    }
+    for (int k = 1; k < nlp; k <<= 1) {
+        if (k < 64) {
+#pragma unroll
+            for (int t = 0; t < 2; t++) v[t] = pymin(v[t], __shfl_xor(v[t], k, 64));
+        } else {   // lanes j and j ^ 64 live in this lane
+            const double a = v[0], b = v[1];
+            v[0] = pymin(a, b);
+            v[1] = pymin(b, a);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+        if (lane + 64 * t < nlp) lds.v[lane + 64 * t] = v[t];
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < DPL; i++) {
+        const int d = min(dbase + i, D - 1);
+        mv[i] = lds.v[d >> 2];
+        mpv[i] = mv[i] + p2;
+    }
+    wave_sync();     // this step's LDS reads before the next step's writes
+}
+
+// One vertical line (column `line`) in the faithful arithmetic, no prefetch: the redo of a
+// column whose costs are not all finite after a pass that folded DU into UD (the fold is exact
+// for finite costs only).  down: UD (penalty ch 2/3) or DU (ch 0/1); accumulate: S += L,
+// else S := f32(0 + L) and the rows the line does not visit are zeroed.
+template <int DPL>
+__device__ __noinline__ void faithful_vertical(const float *cv, const float *pen, float *S, int H, int W, int D,
+                                               int line, bool down, bool accumulate, FaithLds<DPL> &lds)
+{
+    const int lane = threadIdx.x & 63, dbase = lane * DPL;
+    const int n = H - 1 > 2 ? H - 1 : 2;
+    double L[DPL], mv[DPL], mpv[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; i++) L[i] = mv[i] = mpv[i] = 1.0;
+    for (int k = 0; k < n; k++) {
+        const int r = down ? k : H - 1 - k;
+        const int pr = down ? r - 1 : r + 1;
+        const double p1 = (pr >= 0 && pr < H) ? (double)pen[((size_t)pr * W + line) * 16 + (down ? 2 : 0)] : 0.0;
+        const double p2 = (double)pen[((size_t)r * W + line) * 16 + (down ? 3 : 1)];
+        const size_t off = ((size_t)r * W + line) * D;
+        float c[DPL];
+#pragma unroll
+        for (int i = 0; i < DPL; i++) c[i] = cv[off + min(dbase + i, D - 1)];
+        double Ln[DPL];
+        faithful_step<DPL>(Ln, L, c, k == 0, p1, p2, mv, mpv, D, dbase, lds);
+#pragma unroll
+        for (int i = 0; i < DPL; i++) {
+            if (dbase + i < D) {
+                const double s0 = accumulate ? (double)S[off + dbase + i] : 0.0;
+                S[off + dbase + i] = (float)(s0 + Ln[i]);
+            }
+            L[i] = Ln[i];
+        }
+    }
+    if (!accumulate)
+        for (int r = down ? n : 0; down ? r < H : r < H - n; r++)
+#pragma unroll
+            for (int i = 0; i < DPL; i++)
+                if (dbase + i < D) S[((size_t)r * W + line) * D + dbase + i] = 0.0f;
+}
+
 struct SgmSide {
     const float *cv;
     const float *pen;
@@ -260,6 +404,26 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     __shared__ float wbv[WTA ? PF * 64 : 1];
     __shared__ int wba[WTA ? PF * 64 : 1];
     __shared__ int wpx[WTA ? PF : 1];
+    __shared__ FaithLds<DPL> flds;
+
+    if (DU && !FIRST) {
+        // accumulate + DU fold: S's incoming values cannot be recovered after a folded pass, so a
+        // column whose costs are not all finite is found first and runs both directions in the
+        // reference's arithmetic (the fold is exact for finite costs only)
+        bool bad = false;
+        for (int r = 0; r < H && !bad; r++) {
+            float c[DPL];
+            const size_t off = ((size_t)r * W + line) * D;
+#pragma unroll
+            for (int i = 0; i < DPL; i++) c[i] = sd.cv[off + min(dbase + i, D - 1)];
+            bad = any_nonfinite<DPL>(c);
+        }
+        if (bad) {
+            faithful_vertical<DPL>(sd.cv, sd.pen, sd.S, H, W, D, line, true, true, flds);
+            faithful_vertical<DPL>(sd.cv, sd.pen, sd.S, H, W, D, line, false, true, flds);
+            return;
+        }
+    }
 
     // Every load is unconditional (steps past the end re-read a clamped pixel):
     // a predicated load would make the ring slot a phi and force an early wait.
@@ -274,6 +438,8 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
 
     double L[DPL];
     double m = 1.0, mP2 = 1.0;
+    int kf = -1;                   // first step with a non-finite cost: the line continues faithfully
+    bool redo = false;             // DU fold (FIRST): recompute the column in the faithful arithmetic
 #pragma unroll
     for (int i = 0; i < DPL; i++) L[i] = 1.0;
 
@@ -282,6 +448,14 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         for (int j = 0; j < PF; j++) {
             const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
             const Slot<DPL> &sl = ring[j];
+            if (DU) {
+                if (FIRST && !redo) redo = any_nonfinite<DPL>(sl.c);
+            } else if (kf < 0 && k < g.n && any_nonfinite<DPL>(sl.c)) {
+                // every state so far is finite; from step k on the line is redone in the reference's
+                // exact arithmetic after this loop, which stores nothing more for it
+                kf = k;
+            }
+            const bool keep = DU || kf < 0;
             double Ln[DPL];
             if (sl.restart) {
 #pragma unroll
@@ -325,8 +499,8 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 if (lane == 0 && o[0] != o[0]) { bv = -__builtin_inff(); ba = 0; }   // NaN S(0): d = 0
                 wbv[j * 64 + lane] = bv;
                 wba[j * 64 + lane] = ba;
-                if (lane == 0) wpx[j] = k < g.n ? (int)(sl.off / D) : -1;
-            } else if (k < g.n) {
+                if (lane == 0) wpx[j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+            } else if (k < g.n && keep) {
                 if (VEC) {
                     if (dbase < D) {
                         FVec<DPL> ov;
@@ -376,6 +550,48 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
+    if (!DU && kf >= 0) {
+        // the line again in the reference's exact arithmetic (no prefetch: rare path), storing from
+        // step kf on: the replayed finite prefix reproduces the fast steps' state exactly
+        double mv[DPL], mpv[DPL];
+#pragma unroll
+        for (int i = 0; i < DPL; i++) L[i] = mv[i] = mpv[i] = 1.0;
+        for (int k = 0; k < g.n; k++) {
+            int r, c;
+            bool restart;
+            path_pixel(g, line, k, r, c, restart);
+            const int pr = r - g.dr, pc = c - g.dc;
+            const bool pin = pr >= 0 && pr < H && pc >= 0 && pc < W;
+            const double p1 = pin ? (double)sd.pen[((size_t)pr * W + pc) * 16 + g.ch] : 0.0;
+            const double p2 = (double)sd.pen[((size_t)r * W + c) * 16 + g.ch + 1];
+            const size_t off = ((size_t)r * W + c) * D;
+            float cc[DPL];
+#pragma unroll
+            for (int i = 0; i < DPL; i++) cc[i] = sd.cv[off + min(dbase + i, D - 1)];
+            double Ln[DPL];
+            faithful_step<DPL>(Ln, L, cc, restart, p1, p2, mv, mpv, D, dbase, flds);
+            if (k < kf) {
+#pragma unroll
+                for (int i = 0; i < DPL; i++) L[i] = Ln[i];
+                continue;
+            }
+            float o[DPL];
+#pragma unroll
+            for (int i = 0; i < DPL; i++) {
+                const double s0 = FIRST ? 0.0 : (double)sd.S[off + min(dbase + i, D - 1)];
+                o[i] = (float)(s0 + Ln[i]);
+                L[i] = Ln[i];
+            }
+            if (WTA) {
+                const int a = wta_pixel<DPL>(o, dbase, D);
+                if (lane == 63) sd.disp[off / D] = (float)a;
+            } else {
+#pragma unroll
+                for (int i = 0; i < DPL; i++)
+                    if (dbase + i < D) sd.S[off + dbase + i] = o[i];
+            }
+        }
+    }
     if (WTA && g.n < nlen) {
         // pixels of this line's direction never visited: the last line position's successor.
         // DU-RL (the reference's last direction) walks rows H-1 .. 1 and never reaches row 0:
@@ -401,13 +617,21 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 if (d < D) {
                     float v = FIRST ? 0.0f : sd.S[off + d];
                     if (DU) {
-                        const double c = (double)sd.cv[off + d];
+                        const float cf = sd.cv[off + d];
+                        if (FIRST) redo |= (__float_as_uint(cf) & 0x7f800000u) == 0x7f800000u;
+                        const double c = (double)cf;
                         v = (float)((double)v + (r == H - 1 ? c : c + 0.0));
                     }
                     sd.S[off + d] = v;
                 }
             }
         }
+    }
+    if (DU && FIRST && __builtin_amdgcn_ballot_w64(redo) != 0) {
+        // a non-finite cost in this column: the folded DU term is not the reference's -- redo UD
+        // (overwrite) and DU (accumulate) in the faithful arithmetic
+        faithful_vertical<DPL>(sd.cv, sd.pen, sd.S, H, W, D, line, true, false, flds);
+        faithful_vertical<DPL>(sd.cv, sd.pen, sd.S, H, W, D, line, false, true, flds);
     }
 }
 
