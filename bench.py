@@ -5,16 +5,20 @@
                     [--mode pairdp|dshard] [--no-cpu-baseline]
 
 A step = one stereo pair through the hot path with inputs resident in HBM:
-u8 images -> z-norm + pad -> MC-CNN-fast tower (5 fp32-MFMA conv layers) on both
-images -> fused exact cost volume + WTA over D disparities -> float32 disparity.
+u8 images -> z-norm + pad -> MC-CNN-fast tower (5 conv layers, f16x3 MFMA at fp32
+accuracy) on both images -> fused certified cost volume + WTA over D disparities
+(bit-identical to the exact NumPy-order path) -> float32 disparity.
 Default workload: the north-star size 1024x1024, D = 192 (BASELINE.json).
 
 N > 1 (one process per GPU under torchrun, RCCL):
   pairdp : every rank matches its own pair each step (config 4) -- weak scaling,
            no collective on the data path;
   dshard : one pair per step, disparity-sharded over the ranks with the feature
-           row-band all-gather and the (min, argmin) all-gather (config 5) --
-           strong scaling.
+           row-band all-gather and the (min, argmin) all-gather (config 5, the
+           north star's scheme) -- strong scaling;
+  rowband: one pair per step, split by image rows: tower + CV/WTA over all D on
+           each rank's rows, one all-gather of disparity rows (no feature
+           exchange) -- strong scaling.
 
 Rank 0 prints ONE JSON line.  `value` = H*W*D voxels of all pairs of all ranks /
 the max-over-ranks wall time of the K timed steps (Mpixel-disparities/s).
@@ -35,7 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from scenedepthestimation_amd import ops  # noqa: E402
-from scenedepthestimation_amd.parallel import DisparityShardedMatcher, init_from_env  # noqa: E402
+from scenedepthestimation_amd.parallel import DisparityShardedMatcher, RowBandMatcher, init_from_env  # noqa: E402
 from scenedepthestimation_amd.pipeline import StereoMatcher  # noqa: E402
 from scenedepthestimation_amd.synthetic import stereo_pair  # noqa: E402
 
@@ -312,7 +316,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard"])
+    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard", "rowband"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
@@ -337,6 +341,17 @@ def main():
                 t_tower.stop(e)
             return r
         pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
+    elif args.mode == "rowband" and world > 1:
+        rb = RowBandMatcher(H, W, D, rank, world, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
+        rb.load_images(left, right)
+
+        def step(timed=None):
+            e = t_tower.start() if timed == "stages" else None
+            r = rb.match()
+            if e is not None:
+                t_tower.stop(e)
+            return r
+        pairs_per_step, scaling, par = 1, "strong", f"rowband{world}"
     else:
         sgm = what == "tower+cbca+sgm"
         m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode, sgm=sgm,
@@ -493,7 +508,7 @@ def main():
                     "traffic": None,
                     "per_launch": f"{bytes_cv / 1e6:.1f} MB = 4*H*W*(2*64+1) over {cv_ms:.3f} ms" + extra}
     else:
-        stages["dshard_step_ms"] = t_tower.mean_ms()
+        stages[f"{args.mode}_step_ms"] = t_tower.mean_ms()
 
     if roof is not None:
         tb, src = measured_traffic(args.workload)

@@ -13,6 +13,13 @@ The reference has no parallelism; two schemes a
   (strict `<` in rank order == lowest d on ties), so the result is bit-identical
   to WTA1(compute_cost_volume(...)) on one device.
 
+* row-band split (config 5's zero-exchange alternative, ``RowBandMatcher``):
+  rank r owns image rows ``row_band(H, N, r)`` and computes the tower on them
+  (+ halo; bound words all-reduced, 4 B per layer) and the fused cost volume +
+  WTA over ALL disparities for its rows -- a row's costs need only that row of
+  both feature maps, so no feature crosses xGMI; one all-gather of the 4-byte
+  disparity rows assembles the map.  Same bits as one device.
+
 The collectives are plain torch.distributed calls, so the same code runs on
 gloo (CPU tests) and nccl (= RCCL on ROCm).
 """
@@ -151,3 +158,67 @@ class DisparityShardedMatcher:
         _, mn, am = self.m.cost_wta(want=("min", "argmin"))
         mins, args = gather_partials(mn, am, self.world, self.group)
         return ops.argmin_merge(mins, args, out=self.disp)
+
+
+def gather_disparity_rows(band: torch.Tensor, H: int, world: int, out: torch.Tensor | None = None, group=None):
+    """All-gather equal-height [rpb, W] disparity row bands (the last band zero-padded) -> [H, W]."""
+    rpb = band.shape[0]
+    full = torch.empty((world * rpb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
+    dist.all_gather_into_tensor(full, band.contiguous(), group=group)
+    if out is None:
+        return full[:H]
+    out.copy_(full[:H])
+    return out
+
+
+class RowBandMatcher:
+    """Config 5 without a feature exchange: the tower and the fused CV + WTA (all D) on this rank's
+    row band, then one all-gather of the disparity rows.  Per rank at 3840 x 2160, D = 512, N = 8:
+    270 rows of tower + CV/WTA and 1 MB of disparity out, against 3.7 GB of features in for the
+    disparity-sharded scheme."""
+
+    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="f16x3",
+                 cv_mode="certified"):
+        from .pipeline import StereoMatcher
+        self.H, self.W, self.D = H, W, D
+        self.rank, self.world, self.group = rank, world, group
+        self.r0, self.r1, self.rpb = row_band(H, world, rank)
+        self.hb = self.r1 - self.r0
+        L = nlayers
+        # the full images live here (preprocess needs whole-image statistics); the band matcher
+        # holds the band's padded rows, features and workspaces
+        self.full = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, tower_precision=tower_precision,
+                                  cv_mode=cv_mode)
+        self.band = StereoMatcher(max(self.hb, 1), W, D, weights=weights, nlayers=nlayers, nf=nf,
+                                  tower_precision=tower_precision, cv_mode=cv_mode) if self.hb > 0 else None
+        dev = self.full.device
+        self.disp_band = torch.zeros((self.rpb, W), dtype=torch.float32, device=dev)
+        self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
+        self.nlayers = L
+
+    def load_images(self, left_u8, right_u8):
+        self.full.load_images(left_u8, right_u8)
+
+    def features(self):
+        from . import ops
+        from .pipeline import tower_steps
+        f, L = self.full, self.nlayers
+        ops.preprocess_u8_batch(f.img_u82, L, out=f.img_pad2, stats=f.stats2)
+        if self.band is not None:
+            b = self.band
+            b.img_pad2.copy_(f.img_pad2[:, self.r0:self.r1 + 2 * L])
+            for _stage, words in tower_steps(b.img_pad2, b.packed, L, b.feat2, b.ws, b.tower_precision, b.nf):
+                if b.tower_precision == "f16x3":
+                    allreduce_max_(words, self.group)
+            b.split_valid = False
+        elif f.tower_precision == "f16x3":
+            words = torch.zeros((2, 64), dtype=torch.float32, device=f.device)
+            for _ in range(L - 1):
+                allreduce_max_(words, self.group)
+
+    def match(self):
+        self.features()
+        if self.band is not None:
+            self.band.cost_wta()
+            self.disp_band[: self.hb].copy_(self.band.disp)
+        return gather_disparity_rows(self.disp_band, self.H, self.world, out=self.disp, group=self.group)

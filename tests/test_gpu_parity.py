@@ -534,6 +534,35 @@ def test_dshard_matcher_rccl_world1(gpu, oracle):
         dist.destroy_process_group()
 
 
+def test_rowband_matcher_rccl_world1(gpu, oracle):
+    """The row-band matcher's collectives on RCCL (one rank on the single-GPU box)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from scenedepthestimation_amd.parallel import RowBandMatcher
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        H, W, D = 40, 80, 24
+        left, right, _ = stereo_pair(H, W, D, seed=6)
+        rb = RowBandMatcher(H, W, D, 0, 1)
+        rb.load_images(left, right)
+        disp = host(rb.match())
+        m = StereoMatcher(H, W, D)
+        m.load_images(left, right)
+        assert np.array_equal(disp, host(m.match()))
+        fl, fr = host(rb.band.feat[0]), host(rb.band.feat[1])
+        assert np.array_equal(disp, oracle.WTA1(oracle.compute_cost_volume(fl, fr, D)))
+    finally:
+        dist.destroy_process_group()
+
+
 def test_cli_match_single_end_to_end(gpu, tmp_path, monkeypatch):
     from scenedepthestimation_amd import imageio, match_single
     from scenedepthestimation_amd.synthetic import stereo_pair
