@@ -146,6 +146,10 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
 /* sde_tower_layer only, with SDE_TOWER_BF16X6 or SDE_TOWER_F16X3: intermediate activations in the c-block-major
  * layout [nf/16][h][w][16] that sde_tower_forward uses between layers (16-channel blocks
  * contiguous per pixel run).  IN: `in` of a layer >= 3; OUT: `out` of a layer < nlayers. */
+/* With SDE_TOWER_F16X3 only: run the 64 -> 64 layers (3..L) with the Winograd F(2x2, 3x3) kernel
+ * instead of the direct 3x3 kernel (same arithmetic contract and error class, 2.25x fewer MFMA
+ * products, more VALU; slower than the direct kernel at 1024^2 on MI355X -- DESIGN.md 3.2). */
+#define SDE_TOWER_WINOGRAD 16
 #define SDE_TOWER_IN_CBLOCK 2
 #define SDE_TOWER_OUT_CBLOCK 4
 

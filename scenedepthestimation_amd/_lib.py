@@ -26,6 +26,7 @@ SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
 SDE_TOWER_FP32, SDE_TOWER_BF16X6, SDE_TOWER_F16X3 = 0, 1, 8
 SDE_TOWER_IN_CBLOCK, SDE_TOWER_OUT_CBLOCK = 2, 4
+SDE_TOWER_WINOGRAD = 16
 SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
 SDE_SGM_ACCUMULATE = 1
 SDE_SGM_ZERO_DU_PENALTIES = 2

@@ -20,6 +20,8 @@
 //   parts, six partial products on v_mfma_f32_32x32x16_bf16 -- see below.
 #include "sde_common.h"
 
+#include <vector>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -41,7 +43,12 @@ constexpr int LK_W = 9 * NF * NF;                // one [tap][n][c] plane, eleme
 // [mtile 2][cblock 4][tap 9][part 2][lane 64][8] for the F16 variant | F16 header {2^-tau, conv1 L1 bound,
 // max |b1|, 0} (the conv1 terms are used by layer 2, which computes conv1)
 constexpr int LK_F16 = NF + LK_W + 3 * LK_W / 2;   // float offset of the fp16 parts
-constexpr int LK_FLOATS = LK_F16 + LK_W + 4;
+// Winograd F(2x2,3x3) U = G g G^T (tower_wino.h): [xi 16][mtile 2][cblock 4][part 2][lane 64][8] fp16
+// after the F16 header, then its own header {2^-tau_u, 0, 0, 0}
+constexpr int LK_WINO = LK_F16 + LK_W + 4;
+constexpr int LK_WU = 16 * NF * NF * 2;                // fp16 elements
+constexpr int LK_WHDR = LK_WINO + LK_WU / 2;
+constexpr int LK_FLOATS = LK_WHDR + 4;
 
 // float2 slot of channel pair `pair` (0..31) of pixel/row `p` in a swizzled 64-float row
 __device__ __forceinline__ int pslot(int p, int pair) { return p * 32 + (pair ^ (p & 31)); }
@@ -808,6 +815,16 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     }
     __syncthreads();
 
+    uint32_t amax_run = 0u;
+    int amax_img = -1;
+    auto flush_amax = [&]() {
+        if (amax_img < 0) return;
+        uint32_t a = amax_run;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax + amax_img * bt.amax_stride), a);
+        amax_run = 0u;
+    };
     int cur = 0;
     for (; tile < bt.ntiles; tile += gridDim.x) {
         int img, ty0, tx0;
@@ -886,9 +903,13 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                     }
                     if (F16) {
                         if (!xok) amax = 0u;   // lanes past the output edge stored nothing
-#pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) amax = max(amax, (uint32_t)__shfl_xor((int)amax, o, 64));
-                        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax + img * bt.amax_stride), amax);
+                        // one atomic per wave and image (flushed when the tiles move to the next
+                        // image and at the end): every workgroup maxes into the same word
+                        if (img != amax_img) {
+                            flush_amax();
+                            amax_img = img;
+                        }
+                        amax_run = max(amax_run, amax);
                     }
                 } else {
                     // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm.
@@ -981,12 +1002,17 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
             cur ^= 1;
         }
     }
+    if (F16 && !LAST) flush_amax();
     if ((TOWER_DIAG & 128) && tid == 0) {
         const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         out[2 * blockIdx.x] = (float)(t1 - t_start);
         out[2 * blockIdx.x + 1] = (float)(r1 - r_start);
     }
 }
+
+}  // namespace sde
+#include "tower_wino.h"
+namespace sde {
 
 // max |x| over n floats, atomically maxed (as float bits) into *amax (F16 tower scaling):
 // float4 grid-stride loads, one atomic per workgroup.
@@ -1174,6 +1200,42 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
                     for (int q = 0; q < 2; q++)
                         ph[((((size_t)(mt * XP_NCB + cb) * 9 + tap) * 2 + q) * 64 + ln) * 8 + (c & 7)] = parts[q];
                 }
+        {
+            // Winograd U = G g G^T per (n, c) in fp64, scaled by 2^tau_u (max |U| 2^tau_u in [2^14, 2^15)) and
+            // split into two fp16 parts (the residual taken in fp64)
+            static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+            std::vector<double> U((size_t)16 * NF * NF);
+            double umax = 0.0;
+            for (int c = 0; c < NF; c++)
+                for (int n = 0; n < NF; n++) {
+                    double g[3][3];
+                    for (int ky = 0; ky < 3; ky++)
+                        for (int kx = 0; kx < 3; kx++) g[ky][kx] = hwio[l][((size_t)(ky * 3 + kx) * NF + c) * NF + n];
+                    for (int i = 0; i < 4; i++)
+                        for (int j = 0; j < 4; j++) {
+                            double u = 0.0;
+                            for (int ky = 0; ky < 3; ky++)
+                                for (int kx = 0; kx < 3; kx++) u += G[i][ky] * g[ky][kx] * G[j][kx];
+                            U[((size_t)(4 * i + j) * NF + n) * NF + c] = u;
+                            umax = std::max(umax, std::fabs(u));
+                        }
+                }
+            const int tu = (umax > 0.0 && std::isfinite(umax)) ? std::min(std::max(14 - std::ilogb(umax), -100), 100) : 0;
+            _Float16 *pu = reinterpret_cast<_Float16 *>(o + LK_WINO);
+            float *wh = o + LK_WHDR;
+            wh[0] = std::ldexp(1.0f, -tu);
+            wh[1] = wh[2] = wh[3] = 0.0f;
+            for (int xi = 0; xi < 16; xi++)
+                for (int n = 0; n < NF; n++)
+                    for (int c = 0; c < NF; c++) {
+                        const double x = std::ldexp(U[((size_t)xi * NF + n) * NF + c], tu);
+                        const _Float16 h0 = (_Float16)x;
+                        const _Float16 parts[2] = {h0, (_Float16)(x - (double)h0)};
+                        const int mt = n >> 5, cb = c >> 4, ln = ((c >> 3) & 1) * 32 + (n & 31);
+                        for (int q = 0; q < 2; q++)
+                            pu[((((size_t)(xi * 2 + mt) * XP_NCB + cb) * 2 + q) * 64 + ln) * 8 + (c & 7)] = parts[q];
+                    }
+        }
         for (int tap = 0; tap < 9; tap++)
             for (int c = 0; c < NF; c++)
                 for (int n = 0; n < NF; n++) {
@@ -1233,6 +1295,15 @@ static void set_tower_attrs()
     SDE_X6P_ATTR(false, true, false, false);
 #undef SDE_X6P_ATTR1
 #undef SDE_X6P_ATTR
+#define SDE_WINO_ATTR(L, I, O) (void)hipFuncSetAttribute((const void *)wino_kernel<L, I, O>, \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, WN_SMEM)
+    SDE_WINO_ATTR(true, true, false);
+    SDE_WINO_ATTR(true, false, false);
+    SDE_WINO_ATTR(false, true, true);
+    SDE_WINO_ATTR(false, true, false);
+    SDE_WINO_ATTR(false, false, true);
+    SDE_WINO_ATTR(false, false, false);
+#undef SDE_WINO_ATTR
     });
 }
 
@@ -1268,6 +1339,25 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     const float *w1 = packed;
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
+    if (f16 && layer >= 3 && !ohi && !onrm && (flags & SDE_TOWER_WINOGRAD)) {
+        // Winograd F(2x2, 3x3) for the 64 -> 64 layers (tower_wino.h)
+        XpBatch bt;
+        bt.tiles_x = cdiv(wout, WN_TX);
+        bt.tiles_img = bt.tiles_x * cdiv(hout, WN_TY);
+        bt.ntiles = bt.tiles_img * nimg;
+        bt.in_stride = in_stride;
+        bt.out_stride = out_stride;
+        bt.pix_stride = (int64_t)hout * wout;
+        bt.amax_stride = amax_stride;
+        const int grid = std::min(bt.ntiles, cu_count());
+#define SDE_WINO(L, I, O) wino_kernel<L, I, O><<<grid, 512, WN_SMEM, st>>>(in, Hin, Win, wk, out, hout, wout, bt, \
+                                                                          in_amax, out_amax)
+        if (last) { if (in_cb) SDE_WINO(true, true, false); else SDE_WINO(true, false, false); }
+        else if (in_cb) { if (out_cb) SDE_WINO(false, true, true); else SDE_WINO(false, true, false); }
+        else { if (out_cb) SDE_WINO(false, false, true); else SDE_WINO(false, false, false); }
+#undef SDE_WINO
+        return;
+    }
     if (x6) {
         XpBatch bt;
         bt.tiles_x = cdiv(wout, XP_TX);
@@ -1317,6 +1407,10 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 
 static bool tower_flags_ok(int flags, bool layer_api)
 {
+    if (flags & SDE_TOWER_WINOGRAD) {   // F16X3 only: Winograd F(2x2, 3x3) for the 64 -> 64 layers
+        if (!(flags & SDE_TOWER_F16X3)) return false;
+        flags &= ~SDE_TOWER_WINOGRAD;
+    }
     const int prec = flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3);
     if (prec == (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) return false;
     const int layout = SDE_TOWER_IN_CBLOCK | SDE_TOWER_OUT_CBLOCK;

@@ -215,7 +215,9 @@ def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
     return int(lib.sde_tower_workspace_bytes(H, W, nlayers, nf))
 
 
-TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6, "f16x3": _lib.SDE_TOWER_F16X3}
+# "f16x3w": f16x3 with the Winograd F(2x2, 3x3) kernel for layers 3..L (SDE_TOWER_WINOGRAD)
+TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6, "f16x3": _lib.SDE_TOWER_F16X3,
+                    "f16x3w": _lib.SDE_TOWER_F16X3 | _lib.SDE_TOWER_WINOGRAD}
 
 
 def _split_ptrs(split, shape):

@@ -41,7 +41,8 @@ def test_tower_packing_matches_layout():
     packed = ops.pack_tower_weights(hw, hb)
     LW = 9 * 64 * 64
     LF = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 parts
-    LK = LF + LW + 4                              # | 2 fp16 parts of W * 2^tau | F16 header
+    LWINO = LF + LW + 4                           # | 2 fp16 parts of W * 2^tau | F16 header
+    LK = LWINO + 16 * 64 * 64 + 4                 # | 2 fp16 parts of U * 2^tau_u (Winograd) | header
     assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * LK
     assert np.array_equal(packed[:64], hb[0])
     assert np.array_equal(packed[64:640], hw[0].reshape(-1))
@@ -73,6 +74,21 @@ def test_tower_packing_matches_layout():
         scaled = ref.astype(np.float64) * 2.0 ** tau
         assert np.array_equal(hparts[0], scaled.astype(np.float16).astype(np.float64))   # RNE hi part
         assert np.all(np.abs(hparts.sum(0) - scaled) <= np.abs(scaled) * 2.0 ** -22 + 2.0 ** -25)
+        # Winograd F(2x2,3x3): U[xi = 4i + j][n][c] = (G g G^T)[i][j] formed in fp64, scaled by
+        # 2^tau_u (max |U| 2^tau_u in [2^14, 2^15)), two fp16 parts in A-fragment order
+        # [xi 16][mtile 2][cblock 4][part 2][lane 64][8]
+        G = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]])
+        g = hw[l].reshape(3, 3, 64, 64).astype(np.float64)                    # [ky][kx][c][n]
+        U = np.einsum("ia,abcn,jb->ijnc", G, g, G).reshape(16, 64, 64)
+        whdr = packed[base + LWINO + 16 * 64 * 64:base + LK]
+        tau_u = -int(np.log2(whdr[0]))
+        assert whdr[0] == 2.0 ** -tau_u and tuple(whdr[1:]) == (0, 0, 0)
+        assert 2.0 ** 14 <= np.abs(U).max() * 2.0 ** tau_u < 2.0 ** 15
+        u16 = packed[base + LWINO:base + LWINO + 16 * 64 * 64].view(np.float16).reshape(16, 2, 4, 2, 2, 32, 8)
+        uparts = u16.transpose(3, 0, 1, 5, 2, 4, 6).reshape(2, 16, 64, 64).astype(np.float64)
+        uscaled = U * 2.0 ** tau_u
+        assert np.array_equal(uparts[0], uscaled.astype(np.float16).astype(np.float64))
+        assert np.all(np.abs(uparts.sum(0) - uscaled) <= np.abs(uscaled) * 2.0 ** -22 + 2.0 ** -25)
     assert ops.tower_workspace_bytes(100, 80, 5) == 2 * 106 * 86 * 64 * 4 + 256
     assert ops.tower_workspace_bytes(100, 80, 2) == 256
 
@@ -93,6 +109,8 @@ def test_argument_validation_without_gpu():
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 32, 1, N, 0, 0, N, N, N, N) == ERR                 # nf != 64
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, N, 0, 0, N, N, N, N) == -3                  # workspace
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 4, N, N, N, N) == ERR           # bad flags
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 16, N, N, N, N) == ERR          # Winograd w/o f16x3
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 17, N, N, N, N) == ERR          # ... with bf16x6
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 0, 1, N, N, N) == ERR           # hi without lo
     assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 1, 1, 0, N, N, N, N) == ERR                      # layer 1
     assert lib.sde_tower_layer(1, 8, 8, 1, 5, 64, 3, 1, 8, N, N, N, N) == ERR                      # f16x3: bounds

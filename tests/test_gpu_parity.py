@@ -139,7 +139,7 @@ def test_generic_channel_counts(gpu, golden, golden_cases):
 # ----------------------------------------------------------------------------
 # tower
 # ----------------------------------------------------------------------------
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 20, 37), (5, 41, 70), (3, 17, 33), (2, 9, 40), (1, 6, 7)])
 def test_tower_vs_oracle(gpu, oracle, nlayers, H, W, precision):
     from scenedepthestimation_amd import mc_cnn, ops
@@ -167,15 +167,16 @@ def test_tower_precision_report(gpu, oracle):
     ref = oracle.tower_forward(img, hw, hb)
     packed = dev(ops.pack_tower_weights(hw, hb))
     errs = {}
-    for prec in ("fp32", "bf16x6", "f16x3"):
+    for prec in ("fp32", "bf16x6", "f16x3", "f16x3w"):
         out = host(ops.tower_forward(dev(img), packed, L, precision=prec))
         errs[prec] = float(np.abs(out - ref).max())
     print("tower max abs err vs fp64:", errs)
-    assert errs["fp32"] < 1e-5 and errs["bf16x6"] < 1e-5 and errs["f16x3"] < 1e-5
+    assert all(e < 1e-5 for e in errs.values()), errs
 
 
+@pytest.mark.parametrize("precision", ["f16x3", "f16x3w"])
 @pytest.mark.parametrize("scale", [1e-6, 1e-3, 1e3, 1e12])
-def test_tower_f16x3_dynamic_range(gpu, oracle, scale):
+def test_tower_f16x3_dynamic_range(gpu, oracle, scale, precision):
     """f16x3 scales operands by powers of two from device bound words: an image and weights far
     outside fp16's range (tiny or huge) keep fp32-level accuracy (relative to the fp64 tower) and
     never overflow.  The last layer L2-normalises, so the features are scale-free."""
@@ -190,14 +191,14 @@ def test_tower_f16x3_dynamic_range(gpu, oracle, scale):
     img[L:-L, L:-L] = rng.standard_normal((H, W)).astype(np.float32)
     ref = oracle.tower_forward(img, hw, hb)
     packed = dev(ops.pack_tower_weights(hw, hb))
-    out = host(ops.tower_forward(dev(img), packed, L, precision="f16x3"))
+    out = host(ops.tower_forward(dev(img), packed, L, precision=precision))
     assert np.isfinite(out).all()
     err = float(np.abs(out - ref).max())
-    print("f16x3 scale", scale, err)
+    print(precision, "scale", scale, err)
     assert err < 1e-5
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "f16x3"])
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "f16x3w"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 700, 530), (3, 300, 1100), (2, 530, 517)])
 def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W, precision):
     """Sizes with more output tiles than CUs (the persistent bf16x6 kernel's tile loop, partial
@@ -226,7 +227,8 @@ def test_tower_layer_api_matches_forward(gpu):
     packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=9), L)))
     img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
     img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
-    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True), ("f16x3", False), ("f16x3", True)):
+    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True), ("f16x3", False), ("f16x3", True),
+                      ("f16x3w", False), ("f16x3w", True)):
         full = ops.tower_forward(img, packed, L, precision=prec)
         x = img
         words = torch.zeros(L, device="cuda")          # f16x3 bound words, as tower_forward keeps them
@@ -711,7 +713,7 @@ def test_absmax(gpu, off, n):
     assert float(word.cpu()[0]) == want
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w"])
 @pytest.mark.parametrize("nlayers,H,W,N", [(5, 150, 300, 2), (3, 70, 45, 3), (2, 33, 90, 2), (1, 9, 12, 2),
                                            (5, 40, 33, 1)])
 def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
