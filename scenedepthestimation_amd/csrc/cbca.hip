@@ -47,6 +47,11 @@ __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict_
     arms[p] = packed;
 }
 
+// Cache policy of the cost stream (aux bit 1 = nt on gfx950): 1 loads, 2 stores
+#ifndef CBCA_NT
+#define CBCA_NT 0
+#endif
+
 // Buffer descriptor (wave-uniform inputs only) for raw dword loads/stores with a 32-bit
 // per-lane voffset, an SGPR soffset and the hardware range check (voffset >= bytes -> 0 on
 // load, dropped on store).
@@ -119,11 +124,11 @@ __device__ __forceinline__ void cbca_scan(const float *__restrict__ src, float *
     auto issue = [&](int q, int qb, int slot) {
         if (VERT) {
             cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     rc, d4, (int)((uint32_t)(q - qb) * linebytes), 0));
+                                                     rc, d4, (int)((uint32_t)(q - qb) * linebytes), CBCA_NT & 1 ? 2 : 0));
             ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q * W, 0);
             br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, ov4, 4 * q * W, 0);
         } else {
-            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, d4, 4 * q * D, 0));
+            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, d4, 4 * q * D, CBCA_NT & 1 ? 2 : 0));
             ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q, 0);
             uint32_t o4 = SIDE == SDE_SIDE_LEFT ? 4u * (uint32_t)q - d4 : 4u * (uint32_t)q + d4;
             // opaque: the whole offset must reach the range check as voffset.  Left to itself the
@@ -163,7 +168,7 @@ __device__ __forceinline__ void cbca_scan(const float *__restrict__ src, float *
             if (VERT) out = (float)((pb - pa) / (double)(uint16_t)(sN[ib] - sN[ia]));
             else out = (float)(pb - pa);
             const int so = VERT ? (int)((uint32_t)(y - qb) * linebytes) : 4 * y * D;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, d4, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, d4, so, CBCA_NT & 2 ? 2 : 0);
         }
     };
     // V pass: (re)base the cost / output descriptors on row qb; soffsets then stay below

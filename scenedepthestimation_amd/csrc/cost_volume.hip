@@ -176,6 +176,9 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
 //     emission and the barriers.
 // Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
+#ifndef CVLR_NT
+#define CVLR_NT 0     // nontemporal L (1) / R (2) volume stores
+#endif
 #ifndef CVLR_SKIP
 #define CVLR_SKIP 0   // profiling builds only (tools/cvlr_variants.sh): 1 L stores, 2 R stores, 4 dots, 8 loads
 #endif
@@ -303,7 +306,17 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
         if (active && compute && !(CVLR_SKIP & 5)) {
             float *la = outl + (rowvox + (size_t)u) * D + e;
             float *lb = la + D;
-            if (vec) {
+            if (vec && (CVLR_NT & 1)) {
+                typedef float cv_f4 __attribute__((ext_vector_type(4)));
+                if (aok) {
+                    __builtin_nontemporal_store((cv_f4){ca[0], ca[1], ca[2], ca[3]}, reinterpret_cast<cv_f4 *>(la));
+                    __builtin_nontemporal_store((cv_f4){ca[4], ca[5], ca[6], ca[7]}, reinterpret_cast<cv_f4 *>(la) + 1);
+                }
+                if (bok) {
+                    __builtin_nontemporal_store((cv_f4){cb[0], cb[1], cb[2], cb[3]}, reinterpret_cast<cv_f4 *>(lb));
+                    __builtin_nontemporal_store((cv_f4){cb[4], cb[5], cb[6], cb[7]}, reinterpret_cast<cv_f4 *>(lb) + 1);
+                }
+            } else if (vec) {
                 if (aok) {
                     reinterpret_cast<float4 *>(la)[0] = make_float4(ca[0], ca[1], ca[2], ca[3]);
                     reinterpret_cast<float4 *>(la)[1] = make_float4(ca[4], ca[5], ca[6], ca[7]);
@@ -329,7 +342,10 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
         if (!(CVLR_SKIP & 2) && lane < nd) {
             for (int t = wave; t < CV_TX; t += CV_WAVES) {
                 const int xr = q0 - dc - (CV_TX - 1) + t;
-                if (xr >= 0 && xr < W) outr[(rowvox + xr) * D + dc + lane] = rring[cvr_rword(xr, lane)];
+                if (xr >= 0 && xr < W) {
+                    if (CVLR_NT & 2) __builtin_nontemporal_store(rring[cvr_rword(xr, lane)], outr + (rowvox + xr) * D + dc + lane);
+                    else outr[(rowvox + xr) * D + dc + lane] = rring[cvr_rword(xr, lane)];
+                }
             }
         }
         // the next strip's [A] stages its own pixels into the R-ring half these rows occupy:

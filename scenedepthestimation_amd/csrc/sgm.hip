@@ -27,6 +27,18 @@
 // right image sides (the reference's k loop) run in the same launch (grid.y).
 #include "sde_common.h"
 
+#ifndef SGM_DIAG
+#define SGM_DIAG 0    // profiling builds only (tools/build_sgm_variant.sh): 1 loads from a hot 64-pixel region, 2 no S stores
+#endif
+// The cost and S streams are touched once per pass: nontemporal loads and stores (1 | 2).  Both
+// together: 6.44 -> 5.96 ms for the 7-launch pair (either alone: no change; tools/sgm_variants.py).
+#ifndef SGM_NT
+#define SGM_NT 3
+#endif
+#ifndef SGM_FENCE
+#define SGM_FENCE 0   // profiling builds: a scheduling fence between a step's use of its slot and the refill
+#endif
+
 namespace sde {
 
 // direction table in the reference launch order: step (dr, dc) and P1 channel
@@ -78,17 +90,33 @@ __device__ __forceinline__ double dpp_f64(double v)
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-__device__ __forceinline__ double dmin(double a, double t) { return t < a ? t : a; }
+// t < a ? t : a.  VMIN: one v_min_f64 instead of a compare and two selects.  The two differ
+// only when a is NaN or both are zeros of opposite signs.  In the fast recurrence no operand
+// is NaN (non-finite costs and penalties take the faithful path), and a zero's sign never
+// changes a magnitude downstream (x + -0 = x + +0 for x != 0; comparisons ignore it): it can
+// reach S only through S + L with S = -0, and S is never -0 unless the caller's accumulate
+// input holds one -- so the callers that accumulate onto a caller's S keep the selects.
+template <bool VMIN = false>
+__device__ __forceinline__ double dmin(double a, double t)
+{
+    if (VMIN) {
+        double r;
+        asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(t), "v"(a));
+        return r;
+    }
+    return t < a ? t : a;
+}
 
 // min over the 64 lanes, returned wave-uniform
+template <bool VMIN = false>
 __device__ __forceinline__ double wave_min_f64(double v)
 {
-    v = dmin(v, dpp_f64<0xB1>(v));          // quad_perm [1,0,3,2]
-    v = dmin(v, dpp_f64<0x4E>(v));          // quad_perm [2,3,0,1]
-    v = dmin(v, dpp_f64<0x124>(v));         // row_ror:4
-    v = dmin(v, dpp_f64<0x128>(v));         // row_ror:8   -> every lane holds its row's min
-    v = dmin(v, dpp_f64<0x142, 0xA>(v));    // row_bcast:15 -> rows 1, 3
-    v = dmin(v, dpp_f64<0x143, 0xC>(v));    // row_bcast:31 -> row 3 holds all four
+    v = dmin<VMIN>(v, dpp_f64<0xB1>(v));          // quad_perm [1,0,3,2]
+    v = dmin<VMIN>(v, dpp_f64<0x4E>(v));          // quad_perm [2,3,0,1]
+    v = dmin<VMIN>(v, dpp_f64<0x124>(v));         // row_ror:4
+    v = dmin<VMIN>(v, dpp_f64<0x128>(v));         // row_ror:8   -> every lane holds its row's min
+    v = dmin<VMIN>(v, dpp_f64<0x142, 0xA>(v));    // row_bcast:15 -> rows 1, 3
+    v = dmin<VMIN>(v, dpp_f64<0x143, 0xC>(v));    // row_bcast:31 -> row 3 holds all four
     const long long b = __builtin_bit_cast(long long, v);
     const int lo = __builtin_amdgcn_readlane((int)b, 63);
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
@@ -125,6 +153,17 @@ __device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL])
     bool nf = false;
 #pragma unroll
     for (int i = 0; i < DPL; i++) nf |= __builtin_amdgcn_classf(c[i], 0x207);   // s/qNaN, -inf, +inf
+    return __builtin_amdgcn_ballot_w64(nf) != 0;
+}
+
+// ... or a non-finite penalty (the fast recurrence's minima are the reference's for finite
+// operands only)
+template <int DPL>
+__device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL], float p1, float p2)
+{
+    bool nf = __builtin_amdgcn_classf(p1, 0x207) | __builtin_amdgcn_classf(p2, 0x207);
+#pragma unroll
+    for (int i = 0; i < DPL; i++) nf |= __builtin_amdgcn_classf(c[i], 0x207);
     return __builtin_amdgcn_ballot_w64(nf) != 0;
 }
 
@@ -298,9 +337,10 @@ template <int DPL>
 struct Slot {
     float c[DPL];
     float s[DPL];
-    float p1, p2;
+    float p1, p2;   // p1 as loaded: the step applies `pin` (a select at issue would wait for the load)
     size_t off;     // voxel offset of (r, c, d = 0)
     bool restart;
+    bool pin;       // the previous pixel is inside the image (else P1 = 0)
 };
 
 // Incremental walk along a scanline (wave-uniform scalars; no divisions).  Same
@@ -336,19 +376,26 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
                                       Slot<DPL> &sl)
 {
     const int r = min(max(w.r, 0), g.H - 1), c = min(max(w.c, 0), g.W - 1);
-    const size_t px = (size_t)r * g.W + c;
+    const size_t px = (SGM_DIAG & 1) ? (size_t)(c & 63) : (size_t)r * g.W + c;
     int pr = r - g.dr, pc = c - g.dc;
     const bool pin = pr >= 0 && pr < g.H && pc >= 0 && pc < g.W;
     pr = pin ? pr : r;
     pc = pin ? pc : c;
-    const float p1 = sd.pen[((size_t)pr * g.W + pc) * 16 + g.ch];
-    sl.p1 = pin ? p1 : 0.0f;
+    sl.p1 = sd.pen[((size_t)pr * g.W + pc) * 16 + g.ch];
+    sl.pin = pin;
     sl.p2 = sd.pen[px * 16 + g.ch + 1];
     sl.restart = w.restart;
     const size_t off = px * D;
     sl.off = off;
     if (VEC) {
         const size_t o = off + (dbase < D ? dbase : 0);
+        if (SGM_NT & 1) {
+#pragma unroll
+            for (int i = 0; i < DPL; i++) sl.c[i] = __builtin_nontemporal_load(sd.cv + o + i);
+            if (!FIRST)
+#pragma unroll
+                for (int i = 0; i < DPL; i++) sl.s[i] = __builtin_nontemporal_load(sd.S + o + i);
+        } else {
         const FVec<DPL> cv = *reinterpret_cast<const FVec<DPL> *>(sd.cv + o);
 #pragma unroll
         for (int i = 0; i < DPL; i++) sl.c[i] = cv.v[i];
@@ -356,6 +403,7 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
             const FVec<DPL> sv = *reinterpret_cast<const FVec<DPL> *>(sd.S + o);
 #pragma unroll
             for (int i = 0; i < DPL; i++) sl.s[i] = sv.v[i];
+        }
         }
     } else {
 #pragma unroll
@@ -376,7 +424,7 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
 // first-min disparity (rule of WTA_and_SupixelRefinement_kernel) goes to sd.disp instead, and
 // the pixels this direction never visits (its lines stop one short) take the WTA of the S
 // already in memory.
-template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA, int DC, int DIRC>
+template <int DPL, int PF, bool VEC, bool FIRST, bool DU, bool WTA, int DC, int DIRC, bool VMIN>
 __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, int H, int W, int D, int dir)
 {
     // DC != 0: D == DC == 64 * DPL is a compile-time constant -- every lane's disparities are
@@ -448,9 +496,10 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         for (int j = 0; j < PF; j++) {
             const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
             const Slot<DPL> &sl = ring[j];
+            const float p1f = sl.pin ? sl.p1 : 0.0f, p2f = sl.p2;
             if (DU) {
-                if (FIRST && !redo) redo = any_nonfinite<DPL>(sl.c);
-            } else if (kf < 0 && k < g.n && any_nonfinite<DPL>(sl.c)) {
+                if (FIRST && !redo) redo = any_nonfinite<DPL>(sl.c, p1f, p2f);
+            } else if (kf < 0 && k < g.n && any_nonfinite<DPL>(sl.c, p1f, p2f)) {
                 // every state so far is finite; from step k on the line is redone in the reference's
                 // exact arithmetic after this loop, which stores nothing more for it
                 kf = k;
@@ -461,7 +510,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
 #pragma unroll
                 for (int i = 0; i < DPL; i++) Ln[i] = (double)sl.c[i];
             } else {
-                const double p1 = (double)sl.p1;
+                const double p1 = (double)p1f;
                 const double lo = dpp_f64<0x138>(L[DPL - 1]);   // wave_shr:1 -> L'(dbase - 1)
                 const double hi = dpp_f64<0x130>(L[0]);         // wave_shl:1 -> L'(dbase + DPL)
 #pragma unroll
@@ -470,9 +519,9 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     double b = L[i];
                     const double left = i > 0 ? L[i - 1] : lo;
                     const double right = i < DPL - 1 ? L[i + 1] : hi;
-                    if (d > 0) { const double t = left + p1; b = t < b ? t : b; }
-                    if (d < D - 1) { const double t = right + p1; b = t < b ? t : b; }
-                    b = mP2 < b ? mP2 : b;
+                    if (d > 0) b = dmin<VMIN>(b, left + p1);
+                    if (d < D - 1) b = dmin<VMIN>(b, right + p1);
+                    b = dmin<VMIN>(b, mP2);
                     Ln[i] = (double)sl.c[i] + (b - m);
                 }
             }
@@ -500,13 +549,18 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 wbv[j * 64 + lane] = bv;
                 wba[j * 64 + lane] = ba;
                 if (lane == 0) wpx[j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
-            } else if (k < g.n && keep) {
+            } else if (k < g.n && keep && !(SGM_DIAG & 2)) {
                 if (VEC) {
                     if (dbase < D) {
                         FVec<DPL> ov;
 #pragma unroll
                         for (int i = 0; i < DPL; i++) ov.v[i] = o[i];
-                        *reinterpret_cast<FVec<DPL> *>(sd.S + sl.off + dbase) = ov;
+                        if (SGM_NT & 2) {
+#pragma unroll
+                            for (int i = 0; i < DPL; i++) __builtin_nontemporal_store(o[i], sd.S + sl.off + dbase + i);
+                        } else {
+                            *reinterpret_cast<FVec<DPL> *>(sd.S + sl.off + dbase) = ov;
+                        }
                     }
                 } else {
 #pragma unroll
@@ -517,11 +571,14 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             double mm = INF;
 #pragma unroll
             for (int i = 0; i < DPL; i++)
-                if (dbase + i < D) mm = Ln[i] < mm ? Ln[i] : mm;
-            m = wave_min_f64(mm);
-            mP2 = m + (double)sl.p2;
+                if (dbase + i < D) mm = dmin<VMIN>(mm, Ln[i]);
+            m = wave_min_f64<VMIN>(mm);
+            mP2 = m + (double)p2f;
 #pragma unroll
             for (int i = 0; i < DPL; i++) L[i] = Ln[i];
+            // the slot is refilled after its use (not hoisted above it): its registers are reused,
+            // with no moves -- and waits -- at the loop back-edge
+            if (SGM_FENCE) __builtin_amdgcn_sched_barrier(0);
             issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
             ahead.advance(g);
         }
@@ -635,7 +692,10 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     }
 }
 
-template <int DPL, bool VEC, bool FIRST, bool DU, bool WTA>
+// VMIN: S holds no -0.0 on entry (this library wrote it, or the pass overwrites it): the fast
+// recurrence's minima may run on v_min_f64 (see dmin).  The other case (accumulating onto a
+// caller's S) keeps the selects and the generic kernel.
+template <int DPL, bool VEC, bool FIRST, bool DU, bool WTA, bool VMIN>
 static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
                         hipStream_t st)
 {
@@ -643,8 +703,8 @@ static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, i
     const int nlines = horiz ? H : W;
     constexpr int PF = DPL <= 4 ? 8 : 4;
     const dim3 grid(nlines, nsides);
-#define SDE_SGM_LAUNCH(DC, DIRC) sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, DC, DIRC><<<grid, 64, 0, st>>>(a, b, H, W, D, dir)
-    if constexpr (!VEC) {
+#define SDE_SGM_LAUNCH(DC, DIRC) sgm_scan_kernel<DPL, PF, VEC, FIRST, DU, WTA, DC, DIRC, VMIN><<<grid, 64, 0, st>>>(a, b, H, W, D, dir)
+    if constexpr (!VEC || !VMIN) {
         SDE_SGM_LAUNCH(0, -1);
     } else {
     if (D != 64 * DPL) {
@@ -680,42 +740,51 @@ static void launch_scan(const SgmSide &a, const SgmSide &b, int nsides, int H, i
 // 4 accumulate + fused WTA (the last direction)
 template <int DPL, bool VEC>
 static void launch_mode(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, int mode,
-                        hipStream_t st)
+                        bool vmin, hipStream_t st)
 {
     switch (mode) {
-    case 1: launch_scan<DPL, VEC, true, false, false>(a, b, nsides, H, W, D, dir, st); break;
-    case 2: launch_scan<DPL, VEC, true, true, false>(a, b, nsides, H, W, D, dir, st); break;
-    case 3: launch_scan<DPL, VEC, false, true, false>(a, b, nsides, H, W, D, dir, st); break;
-    case 4: launch_scan<DPL, VEC, false, false, true>(a, b, nsides, H, W, D, dir, st); break;
-    default: launch_scan<DPL, VEC, false, false, false>(a, b, nsides, H, W, D, dir, st); break;
+    case 1: launch_scan<DPL, VEC, true, false, false, true>(a, b, nsides, H, W, D, dir, st); break;
+    case 2: launch_scan<DPL, VEC, true, true, false, true>(a, b, nsides, H, W, D, dir, st); break;
+    case 3:
+        if (vmin) launch_scan<DPL, VEC, false, true, false, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, VEC, false, true, false, false>(a, b, nsides, H, W, D, dir, st);
+        break;
+    case 4:
+        if (vmin) launch_scan<DPL, VEC, false, false, true, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, VEC, false, false, true, false>(a, b, nsides, H, W, D, dir, st);
+        break;
+    default:
+        if (vmin) launch_scan<DPL, VEC, false, false, false, true>(a, b, nsides, H, W, D, dir, st);
+        else launch_scan<DPL, VEC, false, false, false, false>(a, b, nsides, H, W, D, dir, st);
+        break;
     }
 }
 
 template <int DPL>
 static void launch_dpl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir, int mode,
-                       hipStream_t st)
+                       bool vmin, hipStream_t st)
 {
-    if ((D % DPL) == 0) launch_mode<DPL, true>(a, b, nsides, H, W, D, dir, mode, st);
-    else launch_mode<DPL, false>(a, b, nsides, H, W, D, dir, mode, st);
+    if ((D % DPL) == 0) launch_mode<DPL, true>(a, b, nsides, H, W, D, dir, mode, vmin, st);
+    else launch_mode<DPL, false>(a, b, nsides, H, W, D, dir, mode, vmin, st);
 }
 
 // One direction over one or two sides; first: S := f32(0 + L) (no S read); du (dir 0
 // only): direction DU folded into the same pass; wta: the final S is reduced to the
 // disparity map (sd.disp) instead of being stored (see sgm_scan_kernel).
 static int sgm_direction_impl(const SgmSide &a, const SgmSide &b, int nsides, int H, int W, int D, int dir,
-                              bool first, hipStream_t st, bool du = false, bool wta = false)
+                              bool first, bool vmin, hipStream_t st, bool du = false, bool wta = false)
 {
     const int mode = wta ? 4 : (first ? (du ? 2 : 1) : (du ? 3 : 0));
     if (wta && (first || du)) return SDE_ERR_ARG;
     switch ((D + 63) / 64) {
-    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, mode, st); break;
-    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, mode, st); break;
+    case 1: launch_dpl<1>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 2: launch_dpl<2>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 3: launch_dpl<3>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 4: launch_dpl<4>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 5: launch_dpl<5>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 6: launch_dpl<6>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 7: launch_dpl<7>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
+    case 8: launch_dpl<8>(a, b, nsides, H, W, D, dir, mode, vmin, st); break;
     default: return SDE_ERR_ARG;
     }
     return SDE_OK;
@@ -932,7 +1001,7 @@ SDE_EXPORT int sde_sgm_direction(const float *cv, const float *pen, int H, int W
     if (!cv || !pen || !S || H < 2 || W < 2 || D <= 0 || D > 512 || direction < 0 || direction > 7)
         return SDE_ERR_ARG;
     const SgmSide a{cv, pen, S, nullptr};
-    const int s = sgm_direction_impl(a, a, 1, H, W, D, direction, false, as_stream(stream));
+    const int s = sgm_direction_impl(a, a, 1, H, W, D, direction, false, false, as_stream(stream));
     if (s != SDE_OK) return s;
     return launch_status();
 }
@@ -958,7 +1027,9 @@ static int sgm_pair(const float *cv_l, const float *pen_l, float *S_l, float *di
     for (int dir = 0; dir < 8; dir++) {
         if (dir == 1 && fold_du) continue;                               // applied in the UD pass
         const bool first = dir == 0 && !(flags & SDE_SGM_ACCUMULATE);   // UD: line = column
-        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, st, dir == 0 && fold_du,
+        // the caller's S is accumulated onto (ACCUMULATE): it may hold -0.0 -- no v_min (see dmin)
+        const int s = sgm_direction_impl(a, b, two ? 2 : 1, H, W, D, dir, first, !(flags & SDE_SGM_ACCUMULATE), st,
+                                         dir == 0 && fold_du,
                                          wta && dir == 7);
         if (s != SDE_OK) return s;
     }

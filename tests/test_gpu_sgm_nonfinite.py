@@ -126,3 +126,43 @@ def test_disparity_compute_by_gpu_nonfinite_features(gpu, oracle):
     a, _ = oracle.lr_check(wl, wr)
     assert np.array_equal(dl, oracle.median5(oracle.lrc_fill(wl, a), wl))
     assert np.array_equal(dr, oracle.median5(wr, wr))
+
+
+@pytest.mark.parametrize("H,W,D", [(9, 13, 128), (16, 70, 192), (7, 30, 100)])
+def test_sgm_nonfinite_penalties_vs_oracle(gpu, oracle, H, W, D):
+    """NaN / inf penalties (caller-supplied penalty maps) take the faithful step like non-finite
+    costs: the fast recurrence's minima are the reference's for finite operands only."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(H + D)
+    cv = (rng.standard_normal((H, W, D)) * 0.5).astype(np.float32)
+    img = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    pen = oracle.sgm_penalties(img)
+    pen[H // 2, W // 3, 2] = np.inf
+    pen[1, 2, 7] = np.nan
+    pen[H - 2, W - 3, 10:16] = -np.inf
+    want = oracle.sgm_8path(cv, pen)
+    got = host(ops.sgm_8path(dev(cv), dev(pen)))
+    assert same_s(got, want)
+
+
+def test_sgm_signed_zero_costs_vs_oracle(gpu, oracle):
+    """Costs of -0.0 (the CPU path's invalid voxels, zero feature vectors) and +0.0 mixed: the
+    fast recurrence's minima may order zeros of opposite signs differently from the reference,
+    which changes only zero signs inside L -- S and the disparities are bit-identical."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(4)
+    H, W, D = 24, 40, 192
+    cv = (rng.standard_normal((H, W, D)) * 0.5).astype(np.float32)
+    cv[rng.random(cv.shape) < 0.3] = -0.0
+    cv[rng.random(cv.shape) < 0.3] = 0.0
+    cv[:, :, ::7] = -0.0
+    img = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    pen = oracle.sgm_penalties(img)
+    want = oracle.sgm_8path(cv, pen)
+    got = host(ops.sgm_8path(dev(cv), dev(pen)))
+    assert got.tobytes() == want.tobytes()
+    S = [torch.empty(cv.shape, dtype=torch.float32, device="cuda") for _ in range(2)]
+    dl, dr = ops.sgm_8path_wta_pair(dev(cv), dev(pen), S[0], None, dev(cv), dev(pen), S[1], None,
+                                    zero_du_penalties=True)
+    w = oracle.wta_sgm(want)
+    assert np.array_equal(host(dl), w) and np.array_equal(host(dr), w)

@@ -1,0 +1,84 @@
+"""A/B timing of tools/_var/libsde_*.so (see build_file_variant.sh) against the in-tree library at
+1024^2 x 192: the GPU-path L/R volumes (sde_cost_volume HWD, L|R), one CBCA iteration of both
+sides (sde_cbca_pair), the 7-launch SGM pair (sde_sgm_8path_wta_pair).  Round-robin, median of 5;
+outputs checked bit-identical to the first library's."""
+import ctypes
+import glob
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from scenedepthestimation_amd import _lib, ops  # noqa: E402
+from scenedepthestimation_amd.synthetic import features  # noqa: E402
+
+H, W, D = 1024, 1024, 192
+what = sys.argv[1].split(",") if len(sys.argv) > 1 else ["cvlr", "cbca", "sgm"]
+fl = torch.from_numpy(features(H, W, seed=0)).cuda()
+fr = torch.from_numpy(features(H, W, seed=1)).cuda()
+vol = [torch.empty((H, W, D), device="cuda") for _ in range(4)]
+g = torch.Generator(device="cuda").manual_seed(0)
+img = [torch.rand((H, W), device="cuda", generator=g) for _ in range(2)]
+arms = [ops.cbca_arms(i) for i in img]
+imgu8 = [torch.randint(0, 256, (H, W), device="cuda", generator=g, dtype=torch.uint8) for _ in range(2)]
+pen = [ops.sgm_penalties(i) for i in imgu8]
+disp = [torch.empty((H, W), device="cuda") for _ in range(2)]
+P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+here = os.path.dirname(os.path.abspath(__file__))
+sos = [_lib.LIB] + sorted(glob.glob(os.path.join(here, "_var", "libsde_*.so")))
+libs = []
+for so in sos:
+    lib = ctypes.CDLL(so)
+    lib.sde_cost_volume.argtypes = [P, P, I, I, I, I, I, I, F, P, P, P]
+    lib.sde_cbca_pair.argtypes = [P, P, P, P, P, P, I, I, I, I, I, P]
+    lib.sde_sgm_8path_wta_pair.argtypes = [P] * 8 + [I, I, I, I, P]
+    libs.append((os.path.basename(so), lib))
+s = torch.cuda.current_stream().cuda_stream
+
+
+def run(lib, w):
+    if w == "cvlr":
+        assert lib.sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
+                                   vol[1].data_ptr(), s) == 0
+    elif w == "cbca":
+        assert lib.sde_cbca_pair(vol[0].data_ptr(), vol[2].data_ptr(), vol[1].data_ptr(), vol[3].data_ptr(),
+                                 arms[0].data_ptr(), arms[1].data_ptr(), H, W, D, 14, 1, s) == 0
+    else:
+        assert lib.sde_sgm_8path_wta_pair(vol[0].data_ptr(), pen[0].data_ptr(), vol[2].data_ptr(), disp[0].data_ptr(),
+                                          vol[1].data_ptr(), pen[1].data_ptr(), vol[3].data_ptr(), disp[1].data_ptr(),
+                                          H, W, D, 2, s) == 0
+
+
+def outputs(w):
+    torch.cuda.synchronize()
+    return [t.clone() for t in (vol[:2] if w != "sgm" else disp)]
+
+
+for w in what:
+    ref = None
+    for name, lib in libs:   # correctness: same inputs, same outputs
+        libs[0][1].sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
+                                   vol[1].data_ptr(), s)
+        run(lib, w)
+        o = outputs(w)
+        if ref is None:
+            ref = o
+        print(f"{w}: {name} outputs identical to {libs[0][0]}: {all(torch.equal(a, b) for a, b in zip(o, ref))}",
+              flush=True)
+    times = {n: [] for n, _ in libs}
+    for rnd in range(5):
+        for name, lib in libs:
+            libs[0][1].sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
+                                       vol[1].data_ptr(), s)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                run(lib, w)
+            e1.record()
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / 3)
+    for name, t in times.items():
+        print(f"{w:5s} {name:24s} median {statistics.median(t):7.3f} ms  ({' '.join(f'{x:.3f}' for x in t)})",
+              flush=True)
