@@ -47,9 +47,11 @@ __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict_
     arms[p] = packed;
 }
 
-// Cache policy of the cost stream (aux bit 1 = nt on gfx950): 1 loads, 2 stores
+// Cache policy of the cost stream (aux bit 1 = nt on gfx950): 1 loads, 2 stores.  The volumes are
+// streamed once per pass: nontemporal both ways, 1.513 -> 1.468 ms per pair iteration
+// (tools/lib_variants.py; the arms stay cached -- every line re-reads them).
 #ifndef CBCA_NT
-#define CBCA_NT 0
+#define CBCA_NT 3
 #endif
 
 // Buffer descriptor (wave-uniform inputs only) for raw dword loads/stores with a 32-bit

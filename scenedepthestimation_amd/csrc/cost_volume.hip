@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
 // Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
 #ifndef CVLR_NT
-#define CVLR_NT 0     // nontemporal L (1) / R (2) volume stores
+#define CVLR_NT 0     // nontemporal L (1) / R (2) volume stores: no gain measured (1.158 -> 1.167-1.182 ms)
 #endif
 #ifndef CVLR_SKIP
 #define CVLR_SKIP 0   // profiling builds only (tools/cvlr_variants.sh): 1 L stores, 2 R stores, 4 dots, 8 loads
