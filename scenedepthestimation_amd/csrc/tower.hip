@@ -314,6 +314,10 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
 #ifndef TOWER_DIAG
 #define TOWER_DIAG 0
 #endif
+#ifndef TOWER_NT
+#define TOWER_NT 0     // nontemporal activation loads (1) / output stores (2): slower (the next layer
+                       // re-reads the outputs from cache; layer 231 -> 234 / 242 / 250 us)
+#endif
 
 constexpr int XP_TY = 16, XP_TX = 32;             // output tile
 constexpr int XP_IY = XP_TY + 2, XP_IX = XP_TX + 2;
@@ -410,7 +414,14 @@ __device__ __forceinline__ float4 xp_load(const float *__restrict__ in, int Hin,
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (y < Hin && x < Win) {
         const float4 *in4 = reinterpret_cast<const float4 *>(in);
-        v = IN_CB ? in4[(((size_t)cb * Hin + y) * Win + x) * 4 + chunk] : in4[((size_t)y * Win + x) * 16 + cb * 4 + chunk];
+        const size_t i = IN_CB ? (((size_t)cb * Hin + y) * Win + x) * 4 + chunk : ((size_t)y * Win + x) * 16 + cb * 4 + chunk;
+        if (TOWER_NT & 1) {
+            typedef float xp_f4 __attribute__((ext_vector_type(4)));
+            const xp_f4 t = __builtin_nontemporal_load(reinterpret_cast<const xp_f4 *>(in4) + i);
+            v = make_float4(t.x, t.y, t.z, t.w);
+        } else {
+            v = in4[i];
+        }
     }
     return v;
 }
@@ -674,7 +685,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xp_rsrc(const void *base)
 __device__ __forceinline__ void xp_st4(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
 {
     if (TOWER_DIAG & 16) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(vo), "s"(so));
-    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, (TOWER_NT & 2) ? 2 : 0);
 }
 
 // One c-block for one MFMA wave: 9 taps x 4 output rows = 36 row-steps; each step's B
