@@ -39,8 +39,12 @@ def shard_range(D: int, nshards: int, s: int):
 
 
 def row_band(H: int, nshards: int, s: int):
-    """Equal-height row bands (the last may be short) -> (r0, r1, rows_per_band)."""
+    """Equal-height row bands (the last may be short, trailing ones may be empty) -> (r0, r1,
+    rows_per_band).  Bands start on even rows: the Winograd tower ("f16x3w") computes 2 x 2
+    output blocks aligned to its input's origin, so only an even band start gives every pixel
+    the block position -- and the bits -- it has in the whole image."""
     rpb = (H + nshards - 1) // nshards
+    rpb += rpb & 1
     r0 = min(H, s * rpb)
     return r0, min(H, r0 + rpb), rpb
 

@@ -85,6 +85,28 @@ def test_config_cones_cli_and_matcher(gpu, oracle, tmp_path, monkeypatch):
 # ----------------------------------------------------------------------------
 # north star: 1024 x 1024, D = 192
 # ----------------------------------------------------------------------------
+def test_north_star_winograd_tower_vs_fp64_band(gpu, oracle):
+    """The opt-in Winograd tower (f16x3w) at the north-star size: a 24-row band against the
+    fp64 restatement (<= 1e-5), the whole pair against the direct f16x3 tower (fp32-level)."""
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    H, W, D = 1024, 1024, 192
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    mw = StereoMatcher(H, W, D, tower_precision="f16x3w")
+    mw.load_images(left, right)
+    mw.features()
+    md = StereoMatcher(H, W, D)
+    md.load_images(left, right)
+    md.features()
+    assert float((mw.feat2 - md.feat2).abs().max()) < 2e-6
+    hw, hb = _weights()
+    pad = host(mw.img_pad[0])
+    ref = oracle.tower_forward(pad[500:524 + 10], hw, hb)
+    assert np.abs(host(mw.feat[0])[500:524] - ref).max() < 1e-5
+
+# ----------------------------------------------------------------------------
+# north star: 1024 x 1024, D = 192
+# ----------------------------------------------------------------------------
 def test_north_star_certified_equals_exact_full_map(gpu, oracle):
     from scenedepthestimation_amd import ops
     from scenedepthestimation_amd.pipeline import StereoMatcher
@@ -224,7 +246,7 @@ def _band_features(m, world, precision):
     return full
 
 
-@pytest.mark.parametrize("precision", ["f16x3", "bf16x6", "fp32"])
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x6", "fp32", "f16x3w"])
 @pytest.mark.parametrize("H,W,world", [(150, 300, 3), (97, 64, 8), (40, 70, 2)])
 def test_row_band_tower_bit_identical(gpu, precision, H, W, world):
     """Config 5's sharded tower: bands with all-reduced bound words == the full-image tower."""
