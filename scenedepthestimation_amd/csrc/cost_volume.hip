@@ -355,6 +355,259 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
     }
 }
 
+// ---------------------------------------------------------------------------
+// L and R volumes in one row sweep, LDS-DMA pipelined (C = 64, [H,W,D]) -- the default.
+//
+// The kernel above issues a strip's global loads into registers after its dot loop, so
+// their latency sits between two dot loops at 2 workgroups per CU (PMC: waves waiting
+// 52 %).  Here a 512-thread workgroup (8 waves, the whole CU's LDS) owns (row y, 64-disparity
+// chunk dc) and sweeps the row in 128-pixel strips, and everything a strip needs arrives by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no VALU) issued one whole dot loop ahead:
+//   * other-side rows: two parity sub-rings of 160 rows x 272 B (even rows in one, odd in the
+//     other, so the 16 rows one ds_read_b128 group reads -- 2 apart -- sit in consecutive
+//     padded rows: 16 distinct bank slots, every chunk an immediate offset).  A strip reads
+//     rows [q0-dc-63, q0-dc+127]; the next strip's 128 new rows land in slots no reader of
+//     this strip touches (191 + 128 <= 320);
+//   * own pixels: two parity buffers of 64 padded rows, copied to VGPRs at the strip start;
+//     the next strip's are DMA'd right after that copy;
+//   * a DMA wave-instruction writes 1 KiB contiguously, so a 32-row unit (32 x 17 chunks of
+//     16 B) is 8.5 instructions whose lane s loads chunk s % 17 of row s / 17 (chunk 16 is the
+//     pad: any valid 16 B);
+//   * wave (g, dq) = (w >> 2, w & 3), lane (p, h): own pixels u = q0 + 64g + 2p, u + 1 and
+//     disparities e = dc + 16dq + 8h .. +7: rows o = u+1-e-j, j = 0..8, serve both pixels
+//     (9 LDS rows -> 16 dots, as above);
+//   * every cost lands in a 128 x 64 LDS tile T[pixel][d] (columns XOR-swizzled by
+//     (pixel >> 1) & 31); the next strip emits the tile as full L runs L[y][x][dc..] and
+//     as the R row pieces R[y][x-d][d] it holds (an R row's 64 disparities come from at
+//     most two strips) -- lane = disparity, coalesced;
+//   * per strip: wait for the DMA + barrier; the previous strip's emission (all its tile reads
+//     batched before its stores), the next rows' DMA, the own copy; barrier; the next own
+//     pixels' DMA, dots.  Every global access has a whole dot loop to complete.  The DMA is inline asm (hipcc's wait insertion would
+//     otherwise drain it before every LDS read); barriers are raw s_barrier after lgkmcnt(0).
+// Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
+// ---------------------------------------------------------------------------
+#ifndef CVLR_DMA
+#define CVLR_DMA 1
+#endif
+#ifndef CD_AUX
+#define CD_AUX 0      // cache-policy bits of the volume stores
+#endif
+#ifndef CD_SKIP
+#define CD_SKIP 0     // diagnostic builds only: 1 emission stores, 2 dots, 4 in-loop DMA, 8 own copy,
+                      // 16 R stores, 32 L stores, 64 whole R rows every strip (wrong values)
+#endif
+constexpr int CD_NX = 128;                                // own pixels per strip
+constexpr int CD_RING = 160;                              // rows per parity sub-ring
+constexpr int CD_RB = 272;                                // bytes per padded LDS row
+constexpr size_t CD_RING_BYTES = (size_t)2 * CD_RING * CD_RB;
+constexpr size_t CD_OWN_BYTES = (size_t)2 * 64 * CD_RB;
+constexpr size_t CD_SMEM = CD_RING_BYTES + CD_OWN_BYTES + (size_t)CD_NX * 64 * 4;   // 154,624 B
+
+__device__ __forceinline__ uint32_t cd_lds(const void *p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void cd_dma16(const void *gsrc, uint32_t lds_dst)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// rows gbase + 2i (i = 0..31, clamped into the image) of one feature row -> 32 padded LDS rows
+__device__ __forceinline__ void cd_unit(const float *__restrict__ rowfeat, int W, int gbase, uint32_t lds_unit, int lane)
+{
+    // (an opaque lane copy: the addresses are recomputed per issue, a few VALU, instead of being
+    // hoisted out of the strip loop into registers the dot loop needs)
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int n = 0; n < 9; n++) {
+        const int s = 64 * n + lane;
+        const int i = (s * 3856) >> 16;                 // s / 17 for s < 544
+        const int ch = s - 17 * i;
+        const int g = min(max(gbase + 2 * i, 0), W - 1);
+        const float *src = rowfeat + (size_t)g * 64 + (ch < 16 ? 4 * ch : 0);
+        if (n < 8 || lane < 32) cd_dma16(src, __builtin_amdgcn_readfirstlane(lds_unit + 1024u * n));
+    }
+}
+
+constexpr uint32_t CD_OOB = 0x80000000u;                 // past any row's records
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cd_rsrc(const void *base, uint32_t bytes)
+{
+    const uintptr_t b = (uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ void cd_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restrict__ fl,
+                                                          const float *__restrict__ fr, int H, int W, int D,
+                                                          int nchunks, float invalid, float *__restrict__ outl,
+                                                          float *__restrict__ outr)
+{
+    extern __shared__ __attribute__((aligned(16))) char cd_sm[];
+    const char *ring = cd_sm;
+    const char *own = cd_sm + CD_RING_BYTES;
+    float *T = reinterpret_cast<float *>(cd_sm + CD_RING_BYTES + CD_OWN_BYTES);
+    const uint32_t ring_l = cd_lds(ring), own_l = cd_lds(own);
+
+    const int job = xcd_remap(blockIdx.x, gridDim.x);   // the chunks of a row share an XCD's L2
+    const int y = job / nchunks;
+    const int dc = (job - y * nchunks) * CV_DC;
+    const int nd = min(CV_DC, D - dc);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = wave >> 2, dq = wave & 3;
+    const int p = lane & 31, h = lane >> 5;
+    const int e = dc + 16 * dq + 8 * h;                 // this lane's first disparity
+    const bool active = e < dc + nd;                    // uniform per half-wave
+    const size_t rowvox = (size_t)y * W;
+    const float *flrow = fl + rowvox * 64;
+    const float *frrow = fr + rowvox * 64;
+    const int nstrips = (W - 1 + dc + nd - 1) / CD_NX + 1;
+    // row y of each volume as a buffer (the host guarantees 4 W D < CD_OOB)
+    const __amdgpu_buffer_rsrc_t rl = cd_rsrc(outl + rowvox * D, (uint32_t)W * D * 4u);
+    const __amdgpu_buffer_rsrc_t rr = cd_rsrc(outr + rowvox * D, (uint32_t)W * D * 4u);   // the last strip reaches x = W-1+dc+nd-1
+
+    // a 32-row unit of other-side rows: parity par of the 64-row block at r (a multiple of 64)
+    auto ring_unit = [&](int r, int par) {
+        int k0 = (r >> 1) % CD_RING;
+        if (k0 < 0) k0 += CD_RING;                      // a multiple of 32: the unit does not wrap
+        cd_unit(frrow, W, r + par, ring_l + (uint32_t)(par * CD_RING + k0) * CD_RB, lane);
+    };
+    // a 32-pixel unit of own pixels: parity par of half hf of the strip at q
+    auto own_unit = [&](int q, int hf, int par) {
+        cd_unit(flrow, W, q + 64 * hf + par, own_l + (uint32_t)(par * 64 + 32 * hf) * CD_RB, lane);
+    };
+    // the tile of the strip at qp -> L rows [qp, qp+128) and the R row pieces it holds
+    auto emit = [&](int qp) {
+        // every T read first (one wait), then the stores: the reads' latency is paid once
+        int lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));     // per-strip address arithmetic, not hoisted registers
+        float vl[16], vr[24];
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const int t = wave + 8 * n;
+            vl[n] = T[t * 64 + (lane ^ ((t >> 1) & 31))];
+        }
+#pragma unroll
+        for (int n = 0; n < 24; n++) {
+            const int pp = min(max(wave - 63 + 8 * n + lane, 0), CD_NX - 1);
+            vr[n] = T[pp * 64 + (lane ^ ((pp >> 1) & 31))];
+        }
+        if (CD_SKIP & 1) return;
+        // buffer stores with 32-bit offsets (one VGPR per address); a voxel not to be stored
+        // gets an offset past the row's records, which the range check drops
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            const int x = qp + wave + 8 * n;
+            const uint32_t off = (x < W && lane < nd && !(CD_SKIP & 32)) ? (uint32_t)(x * D + dc + lane) * 4u : CD_OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, off, 0, CD_AUX);
+        }
+#pragma unroll
+        for (int n = 0; n < 24; n++) {
+            const int i = wave - 63 + 8 * n, xr = qp - dc + i, pp = i + lane;
+            const bool ok = i < CD_NX && xr >= 0 && xr < W && ((pp >= 0 && pp < CD_NX) || (CD_SKIP & 64)) && lane < nd &&
+                            !(CD_SKIP & 16);
+            const uint32_t off = ok ? (uint32_t)(xr * D + dc + lane) * 4u : CD_OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n]), rr, off, 0, CD_AUX);
+        }
+    };
+
+    // strip 0's window: rows [-dc-64, 128-dc) (3 blocks x 2 parities) and own pixels [0, 128)
+    for (int un = wave; un < 10; un += 8) {
+        if (un < 6) ring_unit(-dc - 64 + 64 * (un >> 1), un & 1);
+        else own_unit(0, (un - 6) >> 1, (un - 6) & 1);
+    }
+
+    for (int k = 0; k < nstrips; k++) {
+        const int q0 = k * CD_NX;
+        const bool more = k + 1 < nstrips;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this strip's rows and own pixels
+        cd_barrier();                                       // (and the previous strip's tile)
+        if (k > 0) emit(q0 - CD_NX);
+        // the next strip's rows go to slots the previous strip's dots read
+        if (more && wave < 4 && !(CD_SKIP & 4)) ring_unit(q0 + CD_NX - dc + 64 * (wave >> 1), wave & 1);
+        const bool compute = q0 + 64 * g < W;              // wave-uniform
+        const int u = q0 + 64 * g + 2 * p;
+        // own pixels u (even buffer) and u + 1 (odd buffer), row 32g + p of each
+        f32x2 own_a[32], own_b[32];
+        if (active && compute && !(CD_SKIP & 8)) {
+            const f32x4 *sa = reinterpret_cast<const f32x4 *>(own + (size_t)(32 * g + p) * CD_RB);
+            const f32x4 *sb = reinterpret_cast<const f32x4 *>(own + (size_t)(64 + 32 * g + p) * CD_RB);
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const f32x4 va = sa[c], vb = sb[c];
+                own_a[2 * c] = va.xy; own_a[2 * c + 1] = va.zw;
+                own_b[2 * c] = vb.xy; own_b[2 * c + 1] = vb.zw;
+            }
+        }
+        cd_barrier();                                       // the own buffers and the tile are free
+        if (more && wave >= 4 && !(CD_SKIP & 4)) own_unit(q0 + CD_NX, (wave - 4) >> 1, wave & 1);
+        if (active) {
+            const int ta = 64 * g + 2 * p;                  // tile rows ta (pixel u), ta + 1 (u + 1): swizzle p
+            float *Ta = T + ta * 64, *Tb = Ta + 64;
+            const int c0 = e - dc;
+            const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
+            int kb = (obase >> 1) % CD_RING;
+            if (kb < 0) kb += CD_RING;
+            if (compute && !(CD_SKIP & 2)) {
+                const bool aok = u < W, bok = u + 1 < W;
+#pragma unroll
+                for (int j = 0; j < 9; j++) {
+                    const int o = obase - j;
+                    int kj = kb - (j >> 1);
+                    if (kj < 0) kj += CD_RING;
+                    const f32x4 *row = reinterpret_cast<const f32x4 *>(
+                        ring + (size_t)(((j & 1) ? 0 : CD_RING) + kj) * CD_RB);
+                    f32x2 xa[4], xb[4];     // accumulators (0,1) (2,3) (4,5) (6,7)
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        const f32x4 a = row[2 * m], b = row[2 * m + 1];
+                        const f32x2 r[4] = {a.xy, a.zw, b.xy, b.zw};
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            if (j <= 7) {
+                                const f32x2 pr = own_b[4 * m + t] * r[t];
+                                xb[t] = m == 0 ? pr : xb[t] + pr;
+                            }
+                            if (j >= 1) {
+                                const f32x2 pr = own_a[4 * m + t] * r[t];
+                                xa[t] = m == 0 ? pr : xa[t] + pr;
+                            }
+                        }
+                    }
+                    if (j <= 7) {
+                        const float s = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
+                                        ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
+                        Tb[(c0 + j) ^ p] = (bok && o >= 0) ? -(0.0f + s) : invalid;
+                    }
+                    if (j >= 1) {
+                        const float s = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
+                                        ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
+                        Ta[(c0 + j - 1) ^ p] = (aok && o >= 0) ? -(0.0f + s) : invalid;
+                    }
+                }
+            } else {
+                // past the row end: R's invalid fill only
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    Ta[(c0 + j) ^ p] = invalid;
+                    Tb[(c0 + j) ^ p] = invalid;
+                }
+            }
+        }
+    }
+    cd_barrier();
+    emit((nstrips - 1) * CD_NX);
+}
+
 // Any channel count: one lane per (pixel, d-range), features read from global
 // memory, NumPy's full pairwise recursion.  Correctness path for C != 64.
 template <int OUT>
@@ -769,12 +1022,18 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
             bool ok = true;
             once_per_device(attr, [&ok] {
                 ok = hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess;
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess &&
+                     hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_dma_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CD_SMEM) == hipSuccess;
             });
             if (!ok) return SDE_ERR_LAUNCH;
             const int nchunks = cdiv(D, CV_DC);
-            cvlr_row_kernel<<<dim3((unsigned)(nchunks * H)), 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
-                                                                         out_left, out_right);
+            if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB)
+                cvlr_dma_kernel<<<dim3((unsigned)(nchunks * H)), 512, CD_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
+                                                                             out_left, out_right);
+            else
+                cvlr_row_kernel<<<dim3((unsigned)(nchunks * H)), 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks,
+                                                                             invalid, out_left, out_right);
         } else {
             if (sides & SDE_SIDE_LEFT)
                 cv64_kernel<SDE_SIDE_LEFT, OUT_HWD><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,

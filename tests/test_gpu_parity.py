@@ -111,7 +111,8 @@ def test_hwd_volumes_vs_oracle(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(11)
     for (H, W, D) in [(3, 90, 64), (2, 70, 128), (2, 40, 100), (4, 300, 192), (2, 130, 200), (3, 64, 1),
-                      (2, 1, 5), (2, 5, 64), (2, 128, 67), (1, 200, 130), (2, 63, 250), (1, 257, 190)]:
+                      (2, 1, 5), (2, 5, 64), (2, 128, 67), (1, 200, 130), (2, 63, 250), (1, 257, 190),
+                      (1, 600, 512), (2, 129, 64), (1, 385, 192), (1, 127, 65), (1, 1100, 2)]:
         fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
         fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
         # one row sweep writes both; NaN-filled outputs catch any voxel it leaves unwritten
