@@ -380,9 +380,10 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
 //     (pixel >> 1) & 31); the next strip emits the tile as full L runs L[y][x][dc..] and
 //     as the R row pieces R[y][x-d][d] it holds (an R row's 64 disparities come from at
 //     most two strips) -- lane = disparity, coalesced;
-//   * per strip: wait for the DMA + barrier; the previous strip's emission (all its tile reads
-//     batched before its stores), the next rows' DMA, the own copy; barrier; the next own
-//     pixels' DMA, dots.  Every global access has a whole dot loop to complete.  The DMA is inline asm (hipcc's wait insertion would
+//   * per strip: wait for the DMA + barrier; the previous strip's tile values this wave stores
+//     read into registers, the next rows' DMA, the own copy; barrier; the next own pixels'
+//     DMA, the dots, with the previous strip's stores issued between their rows.  Every global
+//     access has a whole dot loop to complete.  The DMA is inline asm (hipcc's wait insertion would
 //     otherwise drain it before every LDS read); barriers are raw s_barrier after lgkmcnt(0).
 // Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
@@ -486,37 +487,44 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
         cd_unit(flrow, W, q + 64 * hf + par, own_l + (uint32_t)(par * 64 + 32 * hf) * CD_RB, lane);
     };
     // the tile of the strip at qp -> L rows [qp, qp+128) and the R row pieces it holds
-    auto emit = [&](int qp) {
-        // every T read first (one wait), then the stores: the reads' latency is paid once
-        int lane = threadIdx.x & 63;
-        asm volatile("" : "+v"(lane));     // per-strip address arithmetic, not hoisted registers
-        float vl[16], vr[24];
+    // Emission of a strip's tile: emit_load reads every value this wave stores (16 L rows, 24 R
+    // rows; one wait) into registers, so the tile is free at the next barrier; emit_store(qp, j)
+    // issues stores 5j .. 5j+4 of the 40 -- between the dot loop's rows, where the store issue
+    // overlaps the other waves' VALU work.
+    float vl[16], vr[24];
+    auto emit_load = [&]() {
+        int ln = threadIdx.x & 63;
+        asm volatile("" : "+v"(ln));     // per-strip address arithmetic, not hoisted registers
 #pragma unroll
         for (int n = 0; n < 16; n++) {
             const int t = wave + 8 * n;
-            vl[n] = T[t * 64 + (lane ^ ((t >> 1) & 31))];
+            vl[n] = T[t * 64 + (ln ^ ((t >> 1) & 31))];
         }
 #pragma unroll
         for (int n = 0; n < 24; n++) {
-            const int pp = min(max(wave - 63 + 8 * n + lane, 0), CD_NX - 1);
-            vr[n] = T[pp * 64 + (lane ^ ((pp >> 1) & 31))];
+            const int pp = min(max(wave - 63 + 8 * n + ln, 0), CD_NX - 1);
+            vr[n] = T[pp * 64 + (ln ^ ((pp >> 1) & 31))];
         }
+    };
+    // buffer stores with 32-bit offsets (one VGPR per address); a voxel not to be stored gets an
+    // offset past the row's records, which the range check drops
+    auto emit_store = [&](int qp, int j) {
         if (CD_SKIP & 1) return;
-        // buffer stores with 32-bit offsets (one VGPR per address); a voxel not to be stored
-        // gets an offset past the row's records, which the range check drops
+        int ln = threadIdx.x & 63;
+        asm volatile("" : "+v"(ln));
 #pragma unroll
-        for (int n = 0; n < 16; n++) {
-            const int x = qp + wave + 8 * n;
-            const uint32_t off = (x < W && lane < nd && !(CD_SKIP & 32)) ? (uint32_t)(x * D + dc + lane) * 4u : CD_OOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, off, 0, CD_AUX);
-        }
-#pragma unroll
-        for (int n = 0; n < 24; n++) {
-            const int i = wave - 63 + 8 * n, xr = qp - dc + i, pp = i + lane;
-            const bool ok = i < CD_NX && xr >= 0 && xr < W && ((pp >= 0 && pp < CD_NX) || (CD_SKIP & 64)) && lane < nd &&
-                            !(CD_SKIP & 16);
-            const uint32_t off = ok ? (uint32_t)(xr * D + dc + lane) * 4u : CD_OOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n]), rr, off, 0, CD_AUX);
+        for (int n = 5 * j; n < 5 * j + 5 && n < 40; n++) {
+            if (n < 16) {
+                const int x = qp + wave + 8 * n;
+                const uint32_t off = (x < W && ln < nd && !(CD_SKIP & 32)) ? (uint32_t)(x * D + dc + ln) * 4u : CD_OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, off, 0, CD_AUX);
+            } else {
+                const int i = wave - 63 + 8 * (n - 16), xr = qp - dc + i, pp = i + ln;
+                const bool ok = i < CD_NX && xr >= 0 && xr < W && ((pp >= 0 && pp < CD_NX) || (CD_SKIP & 64)) &&
+                                ln < nd && !(CD_SKIP & 16);
+                const uint32_t off = ok ? (uint32_t)(xr * D + dc + ln) * 4u : CD_OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, off, 0, CD_AUX);
+            }
         }
     };
 
@@ -529,9 +537,11 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
     for (int k = 0; k < nstrips; k++) {
         const int q0 = k * CD_NX;
         const bool more = k + 1 < nstrips;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this strip's rows and own pixels
+        // this strip's rows and own pixels (and the previous dot loop's stores: leaving those in
+        // flight with a counted vmcnt(40) measured the same, 1.09-1.13 ms)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cd_barrier();                                       // (and the previous strip's tile)
-        if (k > 0) emit(q0 - CD_NX);
+        if (k > 0) emit_load();
         // the next strip's rows go to slots the previous strip's dots read
         if (more && wave < 4 && !(CD_SKIP & 4)) ring_unit(q0 + CD_NX - dc + 64 * (wave >> 1), wave & 1);
         const bool compute = q0 + 64 * g < W;              // wave-uniform
@@ -550,17 +560,18 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
         }
         cd_barrier();                                       // the own buffers and the tile are free
         if (more && wave >= 4 && !(CD_SKIP & 4)) own_unit(q0 + CD_NX, (wave - 4) >> 1, wave & 1);
-        if (active) {
+        {
             const int ta = 64 * g + 2 * p;                  // tile rows ta (pixel u), ta + 1 (u + 1): swizzle p
             float *Ta = T + ta * 64, *Tb = Ta + 64;
             const int c0 = e - dc;
             const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
             int kb = (obase >> 1) % CD_RING;
             if (kb < 0) kb += CD_RING;
-            if (compute && !(CD_SKIP & 2)) {
-                const bool aok = u < W, bok = u + 1 < W;
+            const bool aok = u < W, bok = u + 1 < W;
+            const bool dots = active && compute && !(CD_SKIP & 2);
 #pragma unroll
-                for (int j = 0; j < 9; j++) {
+            for (int j = 0; j < 9; j++) {
+                if (dots) {
                     const int o = obase - j;
                     int kj = kb - (j >> 1);
                     if (kj < 0) kj += CD_RING;
@@ -584,28 +595,28 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
                         }
                     }
                     if (j <= 7) {
-                        const float s = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
-                                        ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
-                        Tb[(c0 + j) ^ p] = (bok && o >= 0) ? -(0.0f + s) : invalid;
+                        const float sm = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
+                                         ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
+                        Tb[(c0 + j) ^ p] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
                     }
                     if (j >= 1) {
-                        const float s = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
-                                        ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
-                        Ta[(c0 + j - 1) ^ p] = (aok && o >= 0) ? -(0.0f + s) : invalid;
+                        const float sm = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
+                                         ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
+                        Ta[(c0 + j - 1) ^ p] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
                     }
-                }
-            } else {
-                // past the row end: R's invalid fill only
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
+                } else if (active && j < 8) {
+                    // past the row end: R's invalid fill only
                     Ta[(c0 + j) ^ p] = invalid;
                     Tb[(c0 + j) ^ p] = invalid;
                 }
+                if (k > 0) emit_store(q0 - CD_NX, j);     // the previous strip's tile
             }
         }
     }
     cd_barrier();
-    emit((nstrips - 1) * CD_NX);
+    emit_load();
+#pragma unroll
+    for (int j = 0; j < 8; j++) emit_store((nstrips - 1) * CD_NX, j);
 }
 
 // Any channel count: one lane per (pixel, d-range), features read from global
