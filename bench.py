@@ -57,6 +57,7 @@ CBCA_ITERS, CBCA_L1, CBCA_TAU = 2, 14, 0.02
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
 PEAK_BF16_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
+PEAK_VALU_PK_F32_OPS = 78.6   # T ops/s: 256 CUs x 64 lanes x 2 (v_pk_mul/add_f32) x 2.4 GHz, unfused
 PEAK_VALU_F32_TOPS = 78.6     # non-fused f32 ops/s (one op per lane-slot; FMA counts 2 in the 157.3)
 NF = 64
 NLAYERS = 5
@@ -274,10 +275,11 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     out[prefix + "gpu_path_ms"] = path_ms
     out[prefix + "ms_per_pair_tower_plus_gpu_path"] = tower_ms + path_ms
     kern = {}
-    # cvlr_row_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes
+    # cvlr_dma_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes
     ms = _events_ms(lambda: ops.cost_volume(m.feat[0], m.feat[1], D, layout="HWD", right=True, invalid=1.0,
                                             out_left=b["cv"][0], out_right=b["cv"][1]))
-    kern["cvlr_row_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
+    cvlr_ms = ms
+    kern["cvlr_dma_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
     if m.cbca_iters > 0:
         # one CBCA iteration of both sides: H and V pass read + write 4 B/voxel each
         ms = _events_ms(lambda: ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], m.cbca_L1, 1,
@@ -295,6 +297,12 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
         n = m.cbca_iters if k.startswith("cbca") else 1
         tb += byt * n
         tt += ms * n
+    # the L/R volume kernel's other bound: every valid voxel is NumPy's exact fp32 dot product, 64
+    # separately rounded products + 64 adds (pairwise tree, 0.0 + s), on the packed-fp32 VALU
+    k0 = next(iter(per))
+    per[k0]["valu_ops"] = 128.0 * vox
+    per[k0]["valu_frac"] = 128.0 * vox / (cvlr_ms * 1e-3) / (PEAK_VALU_PK_F32_OPS * 1e12)
+    per[k0]["valu_peak"] = f"{PEAK_VALU_PK_F32_OPS} T separately rounded fp32 ops/s (256 CU x 64 lanes x 2 packed x 2.4 GHz)"
     out[prefix + "cv_aggregation_kernels"] = per
     out[prefix + "cv_aggregation_aggregate"] = {
         "ms": tt, "GB": tb / 1e9, "GB_s": tb / (tt * 1e-3) / 1e9, "hbm_frac": tb / (tt * 1e-3) / 1e9 / PEAK_HBM_GBS,

@@ -395,7 +395,9 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
 #endif
 #ifndef CD_SKIP
 #define CD_SKIP 0     // diagnostic builds only: 1 emission stores, 2 dots, 4 in-loop DMA, 8 own copy,
-                      // 16 R stores, 32 L stores, 64 whole R rows every strip (wrong values)
+                      // 16 R stores, 32 L stores, 64 whole R rows every strip (wrong values), 128 per-
+                      // workgroup s_memtime / s_memrealtime deltas into outl[2b], outl[2b+1] (clock probe),
+                      // 256 outputs rotated by a per-workgroup x offset (wrong places: address-pattern probe)
 #endif
 constexpr int CD_NX = 128;                                // own pixels per strip
 constexpr int CD_RING = 160;                              // rows per parity sub-ring
@@ -472,6 +474,9 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
     const float *flrow = fl + rowvox * 64;
     const float *frrow = fr + rowvox * 64;
     const int nstrips = (W - 1 + dc + nd - 1) / CD_NX + 1;
+    const int rot = (CD_SKIP & 256) ? (int)((blockIdx.x * 97u) % (unsigned)W) : 0;   // diagnostic: rotated outputs
+    const uint64_t clk0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t rt0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
     // row y of each volume as a buffer (the host guarantees 4 W D < CD_OOB)
     const __amdgpu_buffer_rsrc_t rl = cd_rsrc(outl + rowvox * D, (uint32_t)W * D * 4u);
     const __amdgpu_buffer_rsrc_t rr = cd_rsrc(outr + rowvox * D, (uint32_t)W * D * 4u);   // the last strip reaches x = W-1+dc+nd-1
@@ -516,13 +521,15 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
         for (int n = 5 * j; n < 5 * j + 5 && n < 40; n++) {
             if (n < 16) {
                 const int x = qp + wave + 8 * n;
-                const uint32_t off = (x < W && ln < nd && !(CD_SKIP & 32)) ? (uint32_t)(x * D + dc + ln) * 4u : CD_OOB;
+                const int xo = (CD_SKIP & 256) ? (x + rot) % W : x;
+                const uint32_t off = (x < W && ln < nd && !(CD_SKIP & 32)) ? (uint32_t)(xo * D + dc + ln) * 4u : CD_OOB;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, off, 0, CD_AUX);
             } else {
                 const int i = wave - 63 + 8 * (n - 16), xr = qp - dc + i, pp = i + ln;
                 const bool ok = i < CD_NX && xr >= 0 && xr < W && ((pp >= 0 && pp < CD_NX) || (CD_SKIP & 64)) &&
                                 ln < nd && !(CD_SKIP & 16);
-                const uint32_t off = ok ? (uint32_t)(xr * D + dc + ln) * 4u : CD_OOB;
+                const int xo = (CD_SKIP & 256) ? (xr + rot) % W : xr;
+                const uint32_t off = ok ? (uint32_t)(xo * D + dc + ln) * 4u : CD_OOB;
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, off, 0, CD_AUX);
             }
         }
@@ -617,6 +624,10 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
     emit_load();
 #pragma unroll
     for (int j = 0; j < 8; j++) emit_store((nstrips - 1) * CD_NX, j);
+    if ((CD_SKIP & 128) && threadIdx.x == 0) {
+        outl[2 * blockIdx.x] = (float)(__builtin_amdgcn_s_memtime() - clk0);
+        outl[2 * blockIdx.x + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
+    }
 }
 
 // Any channel count: one lane per (pixel, d-range), features read from global
