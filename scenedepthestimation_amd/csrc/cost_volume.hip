@@ -376,9 +376,8 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
 //   * wave (g, dq) = (w >> 2, w & 3), lane (p, h): own pixels u = q0 + 64g + 2p, u + 1 and
 //     disparities e = dc + 16dq + 8h .. +7: rows o = u+1-e-j, j = 0..8, serve both pixels
 //     (9 LDS rows -> 16 dots, as above);
-//   * every cost lands in a 128 x 64 LDS tile T[pixel][d] (columns XOR-swizzled by
-//     (pixel >> 1) & 31); the next strip emits the tile as full L runs L[y][x][dc..] and
-//     as the R row pieces R[y][x-d][d] it holds (an R row's 64 disparities come from at
+//   * every cost lands in a 64 x 128 LDS tile T[d][pixel] (stride 129); the next strip emits
+//     the tile as full L runs L[y][x][dc..] and as the R row pieces R[y][x-d][d] it holds (an R row's 64 disparities come from at
 //     most two strips) -- lane = disparity, coalesced;
 //   * per strip: wait for the DMA + barrier; the previous strip's tile values this wave stores
 //     read into registers, the next rows' DMA, the own copy; barrier; the next own pixels'
@@ -395,45 +394,62 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
 #endif
 #ifndef CD_SKIP
 #define CD_SKIP 0     // diagnostic builds only: 1 emission stores, 2 dots, 4 in-loop DMA, 8 own copy,
-                      // 16 R stores, 32 L stores, 64 whole R rows every strip (wrong values), 128 per-
-                      // workgroup s_memtime / s_memrealtime deltas into outl[2b], outl[2b+1] (clock probe),
-                      // 256 outputs rotated by a per-workgroup x offset (wrong places: address-pattern probe)
+                      // 16 R stores, 32 L stores, 128 per-
+                      // workgroup s_memtime / s_memrealtime deltas into outl[2b], outl[2b+1] (clock probe)
 #endif
 constexpr int CD_NX = 128;                                // own pixels per strip
 constexpr int CD_RING = 160;                              // rows per parity sub-ring
 constexpr int CD_RB = 272;                                // bytes per padded LDS row
 constexpr size_t CD_RING_BYTES = (size_t)2 * CD_RING * CD_RB;
 constexpr size_t CD_OWN_BYTES = (size_t)2 * 64 * CD_RB;
-constexpr size_t CD_SMEM = CD_RING_BYTES + CD_OWN_BYTES + (size_t)CD_NX * 64 * 4;   // 154,624 B
+constexpr int CD_TS = CD_NX + 1;                          // tile stride (floats per disparity)
+// the tile (64 x CD_TS floats) + the words an R lane outside the strip may read past its end
+constexpr size_t CD_SMEM = CD_RING_BYTES + CD_OWN_BYTES + (size_t)(64 * CD_TS + 64) * 4;   // 155,392 B
 
 __device__ __forceinline__ uint32_t cd_lds(const void *p)
 {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-__device__ __forceinline__ void cd_dma16(const void *gsrc, uint32_t lds_dst)
+typedef unsigned cd_u32x4 __attribute__((ext_vector_type(4)));
+// raw buffer descriptor of `bytes` bytes at base (SGPRs): loads past the records return zeros
+__device__ __forceinline__ cd_u32x4 cd_desc(const void *base, uint32_t bytes)
+{
+    const uintptr_t b = (uintptr_t)base;
+    cd_u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    r.y = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffffu;
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000u;
+    return r;
+}
+
+// one LDS-DMA wave-instruction: 16 B per lane from byte offset voff of the buffer to lds_dst + 16 lane
+__device__ __forceinline__ void cd_dma16(cd_u32x4 rs, uint32_t voff, uint32_t lds_dst)
 {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
+                 : "v"(voff), "s"(rs), "s"(lds_dst)
                  : "memory");
 }
 
-// rows gbase + 2i (i = 0..31, clamped into the image) of one feature row -> 32 padded LDS rows
-__device__ __forceinline__ void cd_unit(const float *__restrict__ rowfeat, int W, int gbase, uint32_t lds_unit, int lane)
+// rows gbase + 2i (i = 0..31) of a feature row (the buffer) -> 32 padded LDS rows at lds_unit.  Lane
+// s of the 8.5 instructions loads byte 256 (gbase + 2i) + 16 (s - 17 i), i = s / 17 (chunk 16, the
+// pad, takes the next row's chunk 0); rows outside [0, W) -- negative ones wrap to huge offsets --
+// are past the records and load zeros, never used.
+__device__ __forceinline__ void cd_unit(cd_u32x4 rs, int gbase, uint32_t lds_unit, int lane)
 {
-    // (an opaque lane copy: the addresses are recomputed per issue, a few VALU, instead of being
+    // (an opaque lane copy: the offsets are recomputed per issue, a few VALU, instead of being
     // hoisted out of the strip loop into registers the dot loop needs)
     asm volatile("" : "+v"(lane));
+    const uint32_t rowoff = (uint32_t)gbase * 256u;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_unit);
 #pragma unroll
     for (int n = 0; n < 9; n++) {
-        const int s = 64 * n + lane;
-        const int i = (s * 3856) >> 16;                 // s / 17 for s < 544
-        const int ch = s - 17 * i;
-        const int g = min(max(gbase + 2 * i, 0), W - 1);
-        const float *src = rowfeat + (size_t)g * 64 + (ch < 16 ? 4 * ch : 0);
-        if (n < 8 || lane < 32) cd_dma16(src, __builtin_amdgcn_readfirstlane(lds_unit + 1024u * n));
+        const int sl = 64 * n + lane;
+        const int i = (sl * 3856) >> 16;                // sl / 17 for sl < 544
+        if (n < 8 || lane < 32) cd_dma16(rs, rowoff + 16u * sl + 240u * i, lb + 1024u * n);
     }
 }
 
@@ -471,10 +487,9 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
     const int e = dc + 16 * dq + 8 * h;                 // this lane's first disparity
     const bool active = e < dc + nd;                    // uniform per half-wave
     const size_t rowvox = (size_t)y * W;
-    const float *flrow = fl + rowvox * 64;
-    const float *frrow = fr + rowvox * 64;
+    const cd_u32x4 rs_o = cd_desc(fl + rowvox * 64, (uint32_t)W * 256u);   // own pixels' feature row
+    const cd_u32x4 rs_r = cd_desc(fr + rowvox * 64, (uint32_t)W * 256u);   // other side's
     const int nstrips = (W - 1 + dc + nd - 1) / CD_NX + 1;
-    const int rot = (CD_SKIP & 256) ? (int)((blockIdx.x * 97u) % (unsigned)W) : 0;   // diagnostic: rotated outputs
     const uint64_t clk0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t rt0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
     // row y of each volume as a buffer (the host guarantees 4 W D < CD_OOB)
@@ -485,52 +500,47 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
     auto ring_unit = [&](int r, int par) {
         int k0 = (r >> 1) % CD_RING;
         if (k0 < 0) k0 += CD_RING;                      // a multiple of 32: the unit does not wrap
-        cd_unit(frrow, W, r + par, ring_l + (uint32_t)(par * CD_RING + k0) * CD_RB, lane);
+        cd_unit(rs_r, r + par, ring_l + (uint32_t)(par * CD_RING + k0) * CD_RB, lane);
     };
     // a 32-pixel unit of own pixels: parity par of half hf of the strip at q
     auto own_unit = [&](int q, int hf, int par) {
-        cd_unit(flrow, W, q + 64 * hf + par, own_l + (uint32_t)(par * 64 + 32 * hf) * CD_RB, lane);
+        cd_unit(rs_o, q + 64 * hf + par, own_l + (uint32_t)(par * 64 + 32 * hf) * CD_RB, lane);
     };
     // the tile of the strip at qp -> L rows [qp, qp+128) and the R row pieces it holds
     // Emission of a strip's tile: emit_load reads every value this wave stores (16 L rows, 24 R
     // rows; one wait) into registers, so the tile is free at the next barrier; emit_store(qp, j)
-    // issues stores 5j .. 5j+4 of the 40 -- between the dot loop's rows, where the store issue
-    // overlaps the other waves' VALU work.
+    // issues stores 5j .. 5j+4 of the 40 between the dot loop's rows.  The tile is d-major,
+    // T[d * CD_TS + pixel]: lane d's L value of row t is T[d CD_TS + t] and its R value of row i is
+    // T[d (CD_TS + 1) + i] -- one base register each and immediate offsets (8 rows apart = 32 B);
+    // an R lane outside the strip reads a neighbouring word and is not stored.  A store's offset
+    // is the lane's 4 d (past the records for d >= nd or a lane outside the strip: dropped by the
+    // range check) and the row's 4 (x D + dc) in soffset; rows outside the image are skipped.
     float vl[16], vr[24];
+    const float *tl = T + lane * CD_TS + wave;
+    const float *tr = T + lane * (CD_TS + 1) + wave - 63;
+    const uint32_t voff_l = lane < nd ? 4u * lane : CD_OOB;
     auto emit_load = [&]() {
-        int ln = threadIdx.x & 63;
-        asm volatile("" : "+v"(ln));     // per-strip address arithmetic, not hoisted registers
 #pragma unroll
-        for (int n = 0; n < 16; n++) {
-            const int t = wave + 8 * n;
-            vl[n] = T[t * 64 + (ln ^ ((t >> 1) & 31))];
-        }
+        for (int n = 0; n < 16; n++) vl[n] = tl[8 * n];
 #pragma unroll
-        for (int n = 0; n < 24; n++) {
-            const int pp = min(max(wave - 63 + 8 * n + ln, 0), CD_NX - 1);
-            vr[n] = T[pp * 64 + (ln ^ ((pp >> 1) & 31))];
-        }
+        for (int n = 0; n < 24; n++) vr[n] = tr[8 * n];
     };
-    // buffer stores with 32-bit offsets (one VGPR per address); a voxel not to be stored gets an
-    // offset past the row's records, which the range check drops
     auto emit_store = [&](int qp, int j) {
         if (CD_SKIP & 1) return;
-        int ln = threadIdx.x & 63;
-        asm volatile("" : "+v"(ln));
 #pragma unroll
         for (int n = 5 * j; n < 5 * j + 5 && n < 40; n++) {
             if (n < 16) {
                 const int x = qp + wave + 8 * n;
-                const int xo = (CD_SKIP & 256) ? (x + rot) % W : x;
-                const uint32_t off = (x < W && ln < nd && !(CD_SKIP & 32)) ? (uint32_t)(xo * D + dc + ln) * 4u : CD_OOB;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, off, 0, CD_AUX);
+                if (x < W && !(CD_SKIP & 32))
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_l,
+                                                          (x * D + dc) * 4, CD_AUX);
             } else {
-                const int i = wave - 63 + 8 * (n - 16), xr = qp - dc + i, pp = i + ln;
-                const bool ok = i < CD_NX && xr >= 0 && xr < W && ((pp >= 0 && pp < CD_NX) || (CD_SKIP & 64)) &&
-                                ln < nd && !(CD_SKIP & 16);
-                const int xo = (CD_SKIP & 256) ? (xr + rot) % W : xr;
-                const uint32_t off = ok ? (uint32_t)(xo * D + dc + ln) * 4u : CD_OOB;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, off, 0, CD_AUX);
+                const int i = wave - 63 + 8 * (n - 16), xr = qp - dc + i;
+                if (i < CD_NX && xr >= 0 && xr < W && !(CD_SKIP & 16)) {
+                    const uint32_t off = (uint32_t)(i + lane) < (uint32_t)CD_NX ? voff_l : CD_OOB;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, off,
+                                                          (xr * D + dc) * 4, CD_AUX);
+                }
             }
         }
     };
@@ -568,9 +578,8 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
         cd_barrier();                                       // the own buffers and the tile are free
         if (more && wave >= 4 && !(CD_SKIP & 4)) own_unit(q0 + CD_NX, (wave - 4) >> 1, wave & 1);
         {
-            const int ta = 64 * g + 2 * p;                  // tile rows ta (pixel u), ta + 1 (u + 1): swizzle p
-            float *Ta = T + ta * 64, *Tb = Ta + 64;
             const int c0 = e - dc;
+            float *Tw = T + c0 * CD_TS + 64 * g + 2 * p;    // tile column of pixel u (u + 1: +1), disparity c0
             const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
             int kb = (obase >> 1) % CD_RING;
             if (kb < 0) kb += CD_RING;
@@ -604,17 +613,17 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
                     if (j <= 7) {
                         const float sm = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
                                          ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
-                        Tb[(c0 + j) ^ p] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
+                        Tw[j * CD_TS + 1] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
                     }
                     if (j >= 1) {
                         const float sm = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
                                          ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
-                        Ta[(c0 + j - 1) ^ p] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
+                        Tw[(j - 1) * CD_TS] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
                     }
                 } else if (active && j < 8) {
                     // past the row end: R's invalid fill only
-                    Ta[(c0 + j) ^ p] = invalid;
-                    Tb[(c0 + j) ^ p] = invalid;
+                    Tw[j * CD_TS] = invalid;
+                    Tw[j * CD_TS + 1] = invalid;
                 }
                 if (k > 0) emit_store(q0 - CD_NX, j);     // the previous strip's tile
             }
