@@ -79,6 +79,12 @@ __device__ __forceinline__ float4 rw_load(const float *__restrict__ frrow, int W
     return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+template <int CTRL>
+__device__ __forceinline__ float rw_dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ bool rw_nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
 
 // split one unit into the ring slot's hi/lo planes; the pixel's 16 lanes reduce its squared norm
@@ -95,21 +101,20 @@ __device__ __forceinline__ void rw_store(uint4 *ring, unsigned *tmax, unsigned *
     char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
     *reinterpret_cast<uint2 *>(base) = __builtin_bit_cast(uint2, hv);
     *reinterpret_cast<uint2 *>(base + 256 * 16) = __builtin_bit_cast(uint2, lv);
+    // the pixel's 16 lanes sum their squares by DPP (no LDS round trips): lane ^ 1, lane ^ 2, then the
+    // other quad of the 8 and the other 8 of the row by mirrors -- the partial sums are uniform
+    // within each quad / 8 by then, so every add is the xor-butterfly's add (same bits)
     float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-    ss += __shfl_xor(ss, 1, 64);
-    ss += __shfl_xor(ss, 2, 64);
-    ss += __shfl_xor(ss, 4, 64);
-    ss += __shfl_xor(ss, 8, 64);
-    // squared norms are non-negative: their bit patterns order like unsigned integers
-    unsigned nb = __float_as_uint(ss);
-    nb = max(nb, (unsigned)__shfl_xor((int)nb, 16, 64));
-    nb = max(nb, (unsigned)__shfl_xor((int)nb, 32, 64));
+    ss += rw_dpp<0xB1>(ss);     // quad_perm [1,0,3,2]
+    ss += rw_dpp<0x4E>(ss);     // quad_perm [2,3,0,1]
+    ss += rw_dpp<0x141>(ss);    // row_half_mirror
+    ss += rw_dpp<0x140>(ss);    // row_mirror
+    // squared norms are non-negative: their bit patterns order like unsigned integers; one LDS
+    // max per pixel (lane 16k) instead of a cross-row shuffle reduction
     const bool bad = rw_nonfinite(v.x) || rw_nonfinite(v.y) || rw_nonfinite(v.z) || rw_nonfinite(v.w);
     const uint64_t anybad = __ballot(bad);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(&tmax[slot], nb);
-        if (anybad) atomicOr(&tbad[slot], 1u);
-    }
+    if ((threadIdx.x & 15) == 0) atomicMax(&tmax[slot], __float_as_uint(ss));
+    if ((threadIdx.x & 63) == 0 && anybad) atomicOr(&tbad[slot], 1u);
 }
 
 template <bool WANT_MIN>
