@@ -1128,13 +1128,22 @@ __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restric
     img += (size_t)blockIdx.y * H * W;      // batch: image blockIdx.y
     sums += 2 * blockIdx.y;
     out += (size_t)blockIdx.y * (H + 2 * pad) * Wp;
+    // mean and std once per workgroup (the same double expressions: same bits), not per pixel
+    __shared__ float ms[2];
+    if (threadIdx.x == 0) {
+        const double n = (double)H * W;
+        const double mean_d = (double)sums[0] / n;
+        const double var_d = fmax((double)sums[1] / n - mean_d * mean_d, 0.0);
+        ms[0] = (float)mean_d;
+        ms[1] = (float)sqrt(var_d);
+    }
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)(H + 2 * pad) * Wp) return;
-    const double n = (double)H * W;
-    const double mean_d = (double)sums[0] / n;
-    const double var_d = fmax((double)sums[1] / n - mean_d * mean_d, 0.0);
-    const float mean = (float)mean_d, stdv = (float)sqrt(var_d);
-    const int y = (int)(i / Wp) - pad, x = (int)(i % Wp) - pad;
+    const float mean = ms[0], stdv = ms[1];
+    // the padded image has < 2^31 pixels (checked by sde_preprocess_u8_batch)
+    const int ii = (int)i;
+    const int y = ii / Wp - pad, x = ii % Wp - pad;
     float v = 0.0f;
     if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - mean) / stdv;
     out[i] = v;
@@ -1573,6 +1582,7 @@ SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int
     const int blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(npix, 256 * 4 * 8)));
     image_sums_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(imgs, npix, sums);
     const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
+    if (n >= ((int64_t)1 << 31)) return SDE_ERR_ARG;       // znorm_pad_kernel's 32-bit pixel index
     znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256), nimg), 256, 0, st>>>(imgs, H, W, pad, sums, out_pad);
     return launch_status();
 }
