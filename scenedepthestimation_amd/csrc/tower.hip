@@ -1084,22 +1084,32 @@ __global__ __launch_bounds__(256) void image_sums_kernel(const uint8_t *__restri
     img += blockIdx.y * n;      // batch: image blockIdx.y, its two sums at sums[2 * blockIdx.y]
     sums += 2 * blockIdx.y;
     unsigned long long s = 0, q = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
-        if (i + 3 < n && ((reinterpret_cast<uintptr_t>(img + i) & 3) == 0)) {
-            const uint32_t w = *reinterpret_cast<const uint32_t *>(img + i);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const unsigned v = (w >> (8 * k)) & 255u;
-                s += v;
-                q += v * v;
-            }
-        } else {
-            for (int64_t k = i; k < n && k < i + 4; k++) {
-                const unsigned v = img[k];
-                s += v;
-                q += v * v;
-            }
+    // 16-B loads from the first 16-B boundary on; per load the 16 bytes' sum and sum of squares
+    // by v_dot4_u32_u8 (exact: at most 16 x 255^2 < 2^32), added into 64-bit totals
+    const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)img & 15)) & 15));
+    const int64_t nv = (n - head) / 16;
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(img + head);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+        const uint4 w = v4[i];
+        unsigned ss = __builtin_amdgcn_udot4(w.x, 0x01010101u, 0u, false);
+        ss = __builtin_amdgcn_udot4(w.y, 0x01010101u, ss, false);
+        ss = __builtin_amdgcn_udot4(w.z, 0x01010101u, ss, false);
+        ss = __builtin_amdgcn_udot4(w.w, 0x01010101u, ss, false);
+        unsigned qq = __builtin_amdgcn_udot4(w.x, w.x, 0u, false);
+        qq = __builtin_amdgcn_udot4(w.y, w.y, qq, false);
+        qq = __builtin_amdgcn_udot4(w.z, w.z, qq, false);
+        qq = __builtin_amdgcn_udot4(w.w, w.w, qq, false);
+        s += ss;
+        q += qq;
+    }
+    // the < 16 bytes before the boundary and the < 16 after the last full load: block 0's lanes 0-31
+    if (blockIdx.x == 0 && threadIdx.x < 32) {
+        const int64_t k = threadIdx.x < 16 ? (int64_t)threadIdx.x : head + nv * 16 + (threadIdx.x - 16);
+        if (threadIdx.x < 16 ? k < head : k < n) {
+            const unsigned v = img[k];
+            s += v;
+            q += v * v;
         }
     }
 #pragma unroll
@@ -1579,7 +1589,7 @@ SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int
     if (hipMemsetAsync(sums, 0, (size_t)nimg * 2 * sizeof(unsigned long long), st) != hipSuccess)
         return SDE_ERR_LAUNCH;
     const int64_t npix = (int64_t)H * W;
-    const int blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(npix, 256 * 4 * 8)));
+    const int blocks = (int)std::min<int64_t>(256, std::max<int64_t>(1, cdiv(npix, 256 * 16 * 2)));
     image_sums_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(imgs, npix, sums);
     const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
     if (n >= ((int64_t)1 << 31)) return SDE_ERR_ARG;       // znorm_pad_kernel's 32-bit pixel index
