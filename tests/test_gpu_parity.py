@@ -127,6 +127,32 @@ def test_hwd_volumes_vs_oracle(gpu, oracle):
         assert host(R1).tobytes() == oR.tobytes()
 
 
+def test_hwd_volumes_nonfinite_features(gpu, oracle):
+    """The L/R volume kernel on features holding inf / -inf / NaN (process_functional.py:120-131 takes
+    whatever compute_feature returns): NaN exactly where the oracle has NaN, every other voxel
+    bit-exact, across strip and chunk boundaries."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(21)
+    H, W, D = 3, 300, 192
+    fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
+    fl[0, 10, 5] = np.inf
+    fl[1, 127, 0] = np.nan
+    fl[2, 128, 63] = -np.inf
+    fr[2, 200, 63] = -np.inf
+    fr[0, 5, 7] = np.nan
+    fr[1, 64, 9] = np.inf
+    L = torch.full((H, W, D), float("nan"), device="cuda")
+    R = torch.full((H, W, D), float("nan"), device="cuda")
+    ops.cost_volume(dev(fl), dev(fr), D, layout="HWD", right=True, invalid=1.0, out_left=L, out_right=R)
+    oL, oR = oracle.cost_volume_hwd(fl, fr, D, invalid=1.0)
+    for a, b in ((host(L), oL), (host(R), oR)):
+        na, nb = np.isnan(a), np.isnan(b)
+        assert np.array_equal(na, nb)
+        assert na.any() and np.isinf(b).any()
+        assert a[~na].tobytes() == b[~nb].tobytes()
+
+
 def test_generic_channel_counts(gpu, golden, golden_cases):
     """C != 64 takes the generic kernel (full NumPy pairwise recursion)."""
     from scenedepthestimation_amd import ops
