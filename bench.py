@@ -16,6 +16,8 @@ N > 1 (one process per GPU under torchrun, RCCL):
   dshard : one pair per step, disparity-sharded over the ranks with the feature
            row-band all-gather and the (min, argmin) all-gather (config 5, the
            north star's scheme) -- strong scaling;
+  dshard_rep: the same with the tower replicated on every rank: exactly one
+           collective, the (min, argmin) all-gather -- strong scaling;
   rowband: one pair per step, split by image rows: tower + CV/WTA over all D on
            each rank's rows, one all-gather of disparity rows (no feature
            exchange) -- strong scaling.
@@ -39,7 +41,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from scenedepthestimation_amd import ops  # noqa: E402
-from scenedepthestimation_amd.parallel import DisparityShardedMatcher, RowBandMatcher, init_from_env  # noqa: E402
+from scenedepthestimation_amd.parallel import (DisparityShardedMatcher, ReplicatedDisparityShardedMatcher,  # noqa: E402
+                                                RowBandMatcher, init_from_env)
 from scenedepthestimation_amd.pipeline import StereoMatcher  # noqa: E402
 from scenedepthestimation_amd.synthetic import stereo_pair  # noqa: E402
 
@@ -249,6 +252,27 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
             "sample": f"{rows} of {H} rows x {W} cols x D={D} {desc}, {t:.1f} s"}
 
 
+def numpy_baseline(H, W, D, budget_s=8.0):
+    """The NumPy restatement of the reference's CPU path (oracle/np_restatement.py: the same
+    np.multiply / np.sum / argmin expressions as process_functional.py:48-113, which is what
+    match_single.py:51-53 runs), single-threaded, on a bounded row sample of the workload's
+    features (given; the tower is not in this figure)."""
+    from oracle.np_restatement import compute_cost_volume_np, wta1_np
+    from scenedepthestimation_amd.synthetic import features
+
+    def run(rows):
+        fl, fr = features(rows, W, seed=0), features(rows, W, seed=1)
+        t0 = time.perf_counter()
+        wta1_np(compute_cost_volume_np(fl, fr, D))
+        return time.perf_counter() - t0
+    t1 = run(2) / 2
+    rows = int(max(1, min(H, budget_s / max(t1, 1e-6))))
+    t = run(rows)
+    return {"value": rows * W * D / t / 1e6, "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} of {H} rows x {W} cols x D={D}: compute_cost_volume + WTA1 as the reference's NumPy "
+                      f"expressions (np.multiply + np.sum per disparity, np.argmin), features given, {t:.1f} s"}
+
+
 def _events_ms(fn, reps=3):
     """Mean HIP-event time of fn() on torch's current stream over `reps` calls (after one warm call)."""
     fn()
@@ -279,7 +303,7 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     ms = _events_ms(lambda: ops.cost_volume(m.feat[0], m.feat[1], D, layout="HWD", right=True, invalid=1.0,
                                             out_left=b["cv"][0], out_right=b["cv"][1]))
     cvlr_ms = ms
-    kern["cvlr_dma_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
+    kern["cvlr3_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
     if m.cbca_iters > 0:
         # one CBCA iteration of both sides: H and V pass read + write 4 B/voxel each
         ms = _events_ms(lambda: ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], m.cbca_L1, 1,
@@ -291,9 +315,16 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     kern["sgm_scan_kernel (8 paths + WTA, both sides, 7 launches)"] = (ms, 2 * (76.0 * vox + 4.0 * H * W))
     per = {}
     tb = tt = 0.0
+    tkeys = {"cvlr": "cvlr", "cbca": "cbca_pair_iteration", "sgm_": "sgm_pair"}
     for k, (ms, byt) in kern.items():
         gbs = byt / (ms * 1e-3) / 1e9
         per[k] = {"ms": ms, "GB": byt / 1e9, "GB_s": gbs, "hbm_frac": gbs / PEAK_HBM_GBS}
+        # PMC HBM bytes of the same launch(es) at 1024^2 x 192 (profiles/rNN/traffic.json)
+        tk = next(v for a, v in tkeys.items() if k.startswith(a))
+        tr, src = measured_traffic(tk) if (H, W, D) == (1024, 1024, 192) else (None, None)
+        if tr is not None:
+            per[k]["traffic_GB"] = tr / 1e9
+            per[k]["traffic_source"] = src
         n = m.cbca_iters if k.startswith("cbca") else 1
         tb += byt * n
         tt += ms * n
@@ -327,7 +358,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard", "rowband"])
+    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard", "dshard_rep", "rowband"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3", "f16x3w"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
@@ -352,6 +383,17 @@ def main():
                 t_tower.stop(e)
             return r
         pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
+    elif args.mode == "dshard_rep" and world > 1:
+        dr = ReplicatedDisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
+        dr.load_images(left, right)
+
+        def step(timed=None):
+            e = t_tower.start() if timed == "stages" else None
+            r = dr.match()
+            if e is not None:
+                t_tower.stop(e)
+            return r
+        pairs_per_step, scaling, par = 1, "strong", f"dshard_rep{world}"
     elif args.mode == "rowband" and world > 1:
         rb = RowBandMatcher(H, W, D, rank, world, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
         rb.load_images(left, right)
@@ -403,6 +445,7 @@ def main():
 
     roof = None
     parity = None
+    host_io_ms = None
     stages = {}
     if what == "tower+cbca+sgm" and (args.mode == "pairdp" or world == 1):
         stages["tower_ms_pair"] = t_tower.mean_ms()
@@ -474,16 +517,26 @@ def main():
                 ops.tower_forward(m.img_pad[0], m.packed, NLAYERS, NF, out=m.feat[0], workspace=m.ws,
                                   precision=m.tower_precision)
                 stages[f"tower_{m.tower_precision}_vs_fp32_max_abs"] = float((ref - m.feat[0]).abs().max().item())
-            # the reference's boundary hands over host arrays: host u8 pair in -> host float disparity
-            # out, PCIe copies and synchronisation included (reported beside `value`, never as it)
+            # the reference's boundary hands over host arrays (host u8 images in ->
+            # disparity out): pinned host buffers, async copies on the stream, one synchronisation per
+            # pair; reported beside `value` (resident inputs), never as it
+            hl = torch.from_numpy(np.ascontiguousarray(left)).pin_memory()
+            hr = torch.from_numpy(np.ascontiguousarray(right)).pin_memory()
+            hd = torch.empty((H, W), dtype=torch.float32).pin_memory()
+            st = torch.cuda.current_stream()
+
+            def host_pair():
+                m.img_u8[0].copy_(hl, non_blocking=True)
+                m.img_u8[1].copy_(hr, non_blocking=True)
+                hd.copy_(m.match(), non_blocking=True)
+                st.synchronize()
             for _ in range(2):
-                m.load_images(left, right)
-                m.match().cpu()
+                host_pair()
             t0 = time.perf_counter()
-            for _ in range(5):
-                m.load_images(left, right)
-                m.match().cpu()
-            stages["ms_per_pair_host_io"] = (time.perf_counter() - t0) / 5 * 1e3
+            for _ in range(10):
+                host_pair()
+            host_io_ms = (time.perf_counter() - t0) / 10 * 1e3
+            stages["ms_per_pair_host_io"] = host_io_ms
             # parity, outside the timed region: (1) the hooked layer-by-layer tower the timed steps ran
             # == the one-call sde_tower_forward_batch; (2) the certified map == the exact kernel's
             # over every pixel (and the minimum costs bit for bit)
@@ -536,6 +589,8 @@ def main():
         cpu = cpu_baseline(H, W, D, what)
         cpu["cpu_model"] = cpu_model()
         cpu["host_cpus_visible"] = os.cpu_count()
+        if what in ("tower+cv_wta", "cv_wta"):
+            cpu["numpy_restatement"] = numpy_baseline(H, W, D)
 
     if rank == 0:
         line = {
@@ -552,6 +607,10 @@ def main():
         }
         if parity is not None:
             line["parity"] = parity
+        if host_io_ms is not None:
+            line["ms_per_pair_host_io"] = host_io_ms
+            line["host_io"] = ("host u8 pair in -> host f32 disparity out per pair: pinned buffers, async H2D/D2H "
+                               "copies on the compute stream, one synchronisation (SURVEY.md sec. 8(d)'s ms/pair)")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

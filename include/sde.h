@@ -270,9 +270,11 @@ int sde_sgm_8path(const float *cv, const float *pen, int H, int W, int D, float 
  */
 #define SDE_SGM_ACCUMULATE 1
 /* The caller asserts that penalty channels 0/1 are zero (sde_sgm_penalties never writes
- * them, as the reference's sgm_penelty_kernel) and that the costs are finite: direction
- * DU then reduces to S += C (+0.0 off its first row) and is folded into the UD pass
- * (7 passes instead of 8, same values). */
+ * them, as the reference's sgm_penelty_kernel): direction DU then reduces to S += C (+0.0
+ * off its first row) for finite costs and is folded into the UD pass (7 passes instead of
+ * 8, same values).  A column holding a non-finite cost, or a non-finite UD penalty
+ * (channels 2/3), is detected and recomputed for both directions in the reference's exact
+ * arithmetic, so the fold gives the unfolded values for any costs. */
 #define SDE_SGM_ZERO_DU_PENALTIES 2
 int sde_sgm_8path_pair(const float *cv_l, const float *pen_l, float *S_l, const float *cv_r, const float *pen_r,
                        float *S_r, int H, int W, int D, int flags, void *stream);

@@ -1,0 +1,28 @@
+"""NumPy restatement of the reference's CPU path -- TEST INFRASTRUCTURE / CPU BASELINE ONLY.
+
+The same NumPy expressions as process_functional.py:48-73 (compute_cost_volume: one
+np.multiply + np.sum(axis=-1) over an (H, W-d, C) temporary per disparity, then the sign
+flip) and WTA1 (process_functional.py:96-113) as np.argmin over the disparity axis (the
+reference's triple loop gives the same first minimum when no cost is NaN; the golden
+vectors pin both).  Single-threaded (NumPy runs these element-wise kernels on one core).
+bench.py times it as the "numpy_restatement" beside the C port.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def compute_cost_volume_np(featuresl, featuresr, ndisp):
+    """process_functional.py:48-73 -> f32 [D, H, W]: cv[d, :, d:] = -sum_c fl[:, d:] * fr[:, :W-d]."""
+    fl = np.asarray(featuresl, np.float32)
+    fr = np.asarray(featuresr, np.float32)
+    H, W = fl.shape[:2]
+    cv = np.zeros((ndisp, H, W), np.float32)
+    for d in range(min(ndisp, W)):
+        cv[d, :, d:] = np.sum(np.multiply(fl[:, d:], fr[:, :W - d]), axis=-1)
+    return -1 * cv          # (the reference's :72; -0.0 where nothing was computed)
+
+
+def wta1_np(cost_volume):
+    """process_functional.py:96-113 on [D, H, W] -> f32 [H, W] (first minimum over d)."""
+    return np.argmin(cost_volume, axis=0).astype(np.float32)

@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restric
 // Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
 #ifndef CVLR_DMA
-#define CVLR_DMA 1
+#define CVLR_DMA 2    // 2: cvlr3_kernel (two workgroups per CU), 1: cvlr_dma_kernel, 0: cvlr_row_kernel
 #endif
 #ifndef CD_AUX
 #define CD_AUX 0      // cache-policy bits of the volume stores
@@ -637,6 +637,240 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
         outl[2 * blockIdx.x] = (float)(__builtin_amdgcn_s_memtime() - clk0);
         outl[2 * blockIdx.x + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
     }
+}
+
+// ---------------------------------------------------------------------------
+// L and R volumes in one row sweep, two workgroups per CU (C = 64, [H,W,D]) -- the default.
+//
+// cvlr_dma_kernel above holds the whole CU (155 KB of LDS, 8 waves in lock-step barrier phases):
+// its dot loops stop at every strip boundary while the CU waits (PMC: waves parked 37 % of their
+// cycles, VALU busy ~45 %).  Here a 256-thread workgroup (4 waves, one per SIMD) needs 69 KB of
+// LDS, so two independent workgroups share each CU and one's barrier phases and exposed loads
+// overlap the other's dots.  Workgroup = (row y, 64-disparity chunk dc), 64-pixel strips; the
+// exact NumPy-order arithmetic and the two-pixel blocking are cvlr_dma_kernel's, the mapping is
+// per pixel group: wave w, lane (p, h) = (lane & 7, lane >> 3): own pixels u = q0 + 16w + 2p,
+// u + 1, disparities e = dc + 8h .. +7; rows o = u+1-e-j, j = 0..8, serve both pixels (the 16
+// lanes of a ds_read_b128 group read 12 distinct padded rows in distinct bank slots).
+//   * other-side rows: two parity sub-rings of 64 padded rows (272 B) = the strip's two 64-row
+//     blocks [q0-dc-64, q0-dc+64); after the strip's dots the older block's slots take the next
+//     strip's block by LDS-DMA (that latency is the one the co-resident workgroup covers);
+//   * own pixels: LDS-DMA one strip ahead into two parity buffers of 32 padded pixels (coalesced
+//     1 KiB pieces; as buffer loads straight into VGPRs the 8-fold re-reads of every line through
+//     the texture path cost more than the dots' LDS traffic), copied to VGPRs at the strip start;
+//   * every cost lands in a 64 x 65 LDS tile T[d][pixel] of the strip; at the next strip's start
+//     each wave reads its 16 L rows (full 256-B runs L[y][x][dc..dc+63]) and the 16 R rows the
+//     strip completes (R[y][xr][dc..] = cost(xr + d, d): an R row of the chunk spans at most two
+//     strips) into registers; the part an R row got from the previous strip waits in a register
+//     carry (16 VGPRs, lane = d; row xr belongs to wave (xr + 3) & 3 in every strip), so every
+//     store is a whole 256-B run -- no partial lines; the 32 stores go out in the first four dot
+//     rows and drain while the strip computes;
+//   * per strip: wait for the DMA, barrier, own pixels -> VGPRs and tile -> registers, barrier,
+//     the next own pixels' DMA, dots, barrier, the next rows' DMA.
+// Voxels with x >= W are R's invalid fill; strips past the row end compute nothing.
+// ---------------------------------------------------------------------------
+#ifndef C3_SKIP
+#define C3_SKIP 0     // diagnostic builds only: 2 stores, 4 in-loop DMA, 8 dots
+#endif
+constexpr int C3_NX = 64;                                  // own pixels per strip
+constexpr int C3_RING = 64;                                // rows per parity sub-ring
+constexpr int C3_TS = 65;                                  // tile stride (floats per disparity)
+constexpr size_t C3_RING_BYTES = (size_t)2 * C3_RING * CD_RB;           // 34,816 B
+constexpr size_t C3_OWN_BYTES = (size_t)2 * 32 * CD_RB;                 // 17,408 B
+constexpr size_t C3_TILE_OFF = C3_RING_BYTES + C3_OWN_BYTES + 64 * 4;   // R reads reach 63 floats before T
+constexpr size_t C3_SMEM = C3_TILE_OFF + (size_t)(64 * C3_TS + 64) * 4; // ... and 62 past it: 69,376 B
+
+// instructions [n0, n1) of cd_unit's nine (a 32-row unit split over two waves)
+__device__ __forceinline__ void c3_unit(cd_u32x4 rs, int gbase, uint32_t lds_unit, int lane, int n0, int n1)
+{
+    asm volatile("" : "+v"(lane));
+    const uint32_t rowoff = (uint32_t)gbase * 256u;
+    const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_unit);
+#pragma unroll
+    for (int n = 0; n < 9; n++) {
+        if (n < n0 || n >= n1) continue;
+        const int sl = 64 * n + lane;
+        const int i = (sl * 3856) >> 16;                // sl / 17 for sl < 544
+        if (n < 8 || lane < 32) cd_dma16(rs, rowoff + 16u * sl + 240u * i, lb + 1024u * n);
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                       int H, int W, int D, int nchunks, float invalid,
+                                                       float *__restrict__ outl, float *__restrict__ outr)
+{
+    extern __shared__ __attribute__((aligned(16))) char c3_sm[];
+    const char *ring = c3_sm;
+    const char *own = c3_sm + C3_RING_BYTES;
+    float *T = reinterpret_cast<float *>(c3_sm + C3_TILE_OFF);
+    const uint32_t ring_l = cd_lds(ring), own_l = cd_lds(own);
+
+    const int job = xcd_remap(blockIdx.x, gridDim.x);   // the chunks of a row share an XCD's L2
+    const int y = job / nchunks;
+    const int dc = (job - y * nchunks) * CV_DC;
+    const int nd = min(CV_DC, D - dc);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p = lane & 7, h = lane >> 3;
+    const int e = dc + 8 * h;                           // this lane's first disparity
+    const size_t rowvox = (size_t)y * W;
+    const cd_u32x4 rs_o = cd_desc(fl + rowvox * 64, (uint32_t)W * 256u);   // own pixels' feature row
+    const cd_u32x4 rs_r = cd_desc(fr + rowvox * 64, (uint32_t)W * 256u);   // other side's
+    // row y of each volume (the host guarantees 4 W D < CD_OOB)
+    const __amdgpu_buffer_rsrc_t rl = cd_rsrc(outl + rowvox * D, (uint32_t)W * D * 4u);
+    const __amdgpu_buffer_rsrc_t rr = cd_rsrc(outr + rowvox * D, (uint32_t)W * D * 4u);
+    // strips: the emission after strip k completes R rows [q0-dc-63, q0-dc] (whatever nd), so
+    // the last strip holds x = W-1+dc+63
+    const int nstrips = (W + dc + 62) / C3_NX + 1;
+
+    // a 64-row block of other-side rows at r (a multiple of 64): parity par, instructions [n0, n1)
+    auto ring_unit = [&](int r, int par, int n0, int n1) {
+        int k0 = (r >> 1) % C3_RING;
+        if (k0 < 0) k0 += C3_RING;                      // a multiple of 32: the unit does not wrap
+        c3_unit(rs_r, r + par, ring_l + (uint32_t)(par * C3_RING + k0) * CD_RB, lane, n0, n1);
+    };
+    // own pixels q + par + 2i (i < 32) -> parity buffer par
+    auto own_unit = [&](int q, int par, int n0, int n1) {
+        c3_unit(rs_o, q + par, own_l + (uint32_t)(par * 32) * CD_RB, lane, n0, n1);
+    };
+
+    // Emission of the tile of the strip at qp (lane = disparity dc + lane): L rows x = qp + wave + 4n,
+    // R rows xr = qp - dc - 63 + i, i = 4n + wave (complete after this strip: lanes lane >= 63 - i
+    // from the tile, the others from the carry), and the carry of the R rows this strip starts
+    // (xr + 64, lanes lane <= 62 - i, for the next strip's emission).  Reads outside the tile land
+    // in the slack words and are never selected.
+    float vl[16], vr[16], cr[16];
+#pragma unroll
+    for (int n = 0; n < 16; n++) cr[n] = invalid;
+    const float *tl = T + lane * C3_TS + wave;
+    const float *tr = T + lane * (C3_TS + 1) + wave - 63;
+    const uint32_t voff_d = lane < nd ? 4u * lane : CD_OOB;
+    auto emit_load = [&]() {
+#pragma unroll
+        for (int n = 0; n < 16; n++) {
+            vl[n] = tl[4 * n];
+            const float t = tr[4 * n];
+            vr[n] = lane >= 63 - (4 * n + wave) ? t : cr[n];
+            cr[n] = tr[4 * n + 64];
+        }
+    };
+    // stores 8j .. 8j+7 of the 32 (16 L, 16 R runs), issued in the first four dot rows so they
+    // drain while the strip computes; rows outside the image are skipped
+    auto emit_store = [&](int qp, int j) {
+#pragma unroll
+        for (int n = 8 * j; n < 8 * j + 8 && n < 32; n++) {
+            if (n < 16) {
+                const int x = qp + wave + 4 * n;
+                if (x < W)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d,
+                                                          (x * D + dc) * 4, 0);
+            } else {
+                const int xr = qp - dc - 63 + 4 * (n - 16) + wave;
+                if (xr >= 0 && xr < W)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d,
+                                                          (xr * D + dc) * 4, 0);
+            }
+        }
+    };
+
+    // strip 0: rows [-dc-64, 64-dc) (two blocks x two parities, one unit per wave) and own pixels
+    ring_unit(-dc - 64 + 64 * (wave >> 1), wave & 1, 0, 9);
+    own_unit(0, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
+
+    for (int k = 0; k < nstrips; k++) {
+        const int q0 = k * C3_NX;
+        const bool more = k + 1 < nstrips;
+        const bool compute = q0 + 16 * wave < W;            // wave-uniform
+        const int u = q0 + 16 * wave + 2 * p;
+        // this strip's rows and own pixels have landed (every wave's DMA, hence the barrier); the
+        // previous strip's tile is complete
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        cd_barrier();
+        f32x2 own_a[32], own_b[32];
+        if (compute) {
+            const f32x4 *sa = reinterpret_cast<const f32x4 *>(own + (size_t)(8 * wave + p) * CD_RB);
+            const f32x4 *sb = reinterpret_cast<const f32x4 *>(own + (size_t)(32 + 8 * wave + p) * CD_RB);
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const f32x4 va = sa[c], vb = sb[c];
+                own_a[2 * c] = va.xy; own_a[2 * c + 1] = va.zw;
+                own_b[2 * c] = vb.xy; own_b[2 * c + 1] = vb.zw;
+            }
+        }
+        if (k > 0) emit_load();
+        cd_barrier();                                       // the own buffers and the tile are free
+        if (more && !(C3_SKIP & 4)) own_unit(q0 + C3_NX, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
+        {
+            float *Tw = T + (e - dc) * C3_TS + 16 * wave + 2 * p;   // tile column of pixel u (u + 1: +1), disparity e
+            const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
+            const int kb = (obase >> 1) & (C3_RING - 1);
+            const bool aok = u < W, bok = u + 1 < W;
+            // wave-uniform (lanes past nd compute values that are never stored): no exec masking, so
+            // the nine rows are one straight-line block the scheduler can pipeline across
+            if (compute && !(C3_SKIP & 8)) {
+                // the 72 (row, 32-byte piece) steps with the pieces two steps ahead in flight
+                auto piece = [&](int jj, int mm, f32x4 &a, f32x4 &b) {
+                    const int kj = (kb - (jj >> 1)) & (C3_RING - 1);
+                    const f32x4 *row = reinterpret_cast<const f32x4 *>(
+                        ring + (size_t)(((jj & 1) ? 0 : C3_RING) + kj) * CD_RB);
+                    a = row[2 * mm];
+                    b = row[2 * mm + 1];
+                };
+                f32x4 pa[3], pb[3];
+                piece(0, 0, pa[0], pb[0]);
+                piece(0, 1, pa[1], pb[1]);
+#pragma unroll
+                for (int j = 0; j < 9; j++) {
+                    const int o = obase - j;
+                    f32x2 xa[4], xb[4];     // accumulators (0,1) (2,3) (4,5) (6,7)
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        const int st = 8 * j + m, nx = st + 2;
+                        if (nx < 72) piece(nx >> 3, nx & 7, pa[nx % 3], pb[nx % 3]);
+                        const f32x4 a = pa[st % 3], b = pb[st % 3];
+                        const f32x2 r[4] = {a.xy, a.zw, b.xy, b.zw};
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            if (j <= 7) {
+                                const f32x2 pr = own_b[4 * m + t] * r[t];
+                                xb[t] = m == 0 ? pr : xb[t] + pr;
+                            }
+                            if (j >= 1) {
+                                const f32x2 pr = own_a[4 * m + t] * r[t];
+                                xa[t] = m == 0 ? pr : xa[t] + pr;
+                            }
+                        }
+                    }
+                    if (j <= 7) {
+                        const float sm = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
+                                         ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
+                        Tw[j * C3_TS + 1] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
+                    }
+                    if (j >= 1) {
+                        const float sm = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
+                                         ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
+                        Tw[(j - 1) * C3_TS] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
+                    }
+                    if (k > 0 && !(C3_SKIP & 2)) emit_store(q0 - C3_NX, j);     // the previous strip's runs
+                }
+            } else {
+                // past the row end: R's invalid fill only
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    Tw[j * C3_TS] = invalid;
+                    Tw[j * C3_TS + 1] = invalid;
+                    if (k > 0 && !(C3_SKIP & 2)) emit_store(q0 - C3_NX, j);
+                }
+            }
+        }
+        // every wave's dots are done: the older row block's slots take the next strip's block
+        cd_barrier();
+        if (more && !(C3_SKIP & 4)) ring_unit(q0 + C3_NX - dc, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cd_barrier();
+    emit_load();
+#pragma unroll
+    for (int j = 0; j < 4; j++) emit_store((nstrips - 1) * C3_NX, j);
 }
 
 // Any channel count: one lane per (pixel, d-range), features read from global
@@ -1050,16 +1284,20 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
         } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
             // one row sweep per (row, 64-disparity chunk) writes both volumes
             static std::atomic<uint64_t> attr{0};
-            bool ok = true;
-            once_per_device(attr, [&ok] {
-                ok = hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess &&
-                     hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_dma_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CD_SMEM) == hipSuccess;
+            const bool ok = once_per_device(attr, [] {
+                return hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess &&
+                       hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_dma_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CD_SMEM) == hipSuccess &&
+                       hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr3_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM) == hipSuccess;
             });
             if (!ok) return SDE_ERR_LAUNCH;
             const int nchunks = cdiv(D, CV_DC);
-            if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB)
+            if (CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB)
+                cvlr3_kernel<<<dim3((unsigned)(nchunks * H)), 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
+                                                                          out_left, out_right);
+            else if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB)
                 cvlr_dma_kernel<<<dim3((unsigned)(nchunks * H)), 512, CD_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
                                                                              out_left, out_right);
             else

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "sde.h"
 
@@ -24,19 +25,26 @@ static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // Per-device one-time setup (kernel attributes such as the >64 KB dynamic-LDS opt-in are per
 // device): `done` holds one bit per device id; the first caller on a device runs `fn` and
-// publishes the bit.  Concurrent first calls may both run `fn`, which is idempotent.
+// publishes the bit.  Concurrent first calls may both run `fn`, which is idempotent.  A callback
+// returning bool publishes the bit only on success (a failed setup is retried by the next call,
+// and every call returns whether the setup holds); a void callback always publishes.
 template <typename F>
-static inline void once_per_device(std::atomic<uint64_t> &done, F fn)
+static inline bool once_per_device(std::atomic<uint64_t> &done, F fn)
 {
+    constexpr bool checked = std::is_same<decltype(fn()), bool>::value;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        if constexpr (checked) return fn();
         fn();
-        return;
+        return true;
     }
     const uint64_t bit = 1ull << dev;
-    if (done.load(std::memory_order_acquire) & bit) return;
-    fn();
-    done.fetch_or(bit, std::memory_order_acq_rel);
+    if (done.load(std::memory_order_acquire) & bit) return true;
+    bool ok = true;
+    if constexpr (checked) ok = fn();
+    else fn();
+    if (ok) done.fetch_or(bit, std::memory_order_acq_rel);
+    return ok;
 }
 
 // 64-float (256 B) rows in LDS, XOR-swizzled at 16-B granularity: the 16 lanes

@@ -458,13 +458,15 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         // accumulate + DU fold: S's incoming values cannot be recovered after a folded pass, so a
         // column whose costs are not all finite is found first and runs both directions in the
         // reference's arithmetic (the fold is exact for finite costs only)
+        // (and the UD penalties, channels 2/3: the fast recurrence's minima are the reference's
+        // for finite operands only)
         bool bad = false;
         for (int r = 0; r < H && !bad; r++) {
             float c[DPL];
-            const size_t off = ((size_t)r * W + line) * D;
+            const size_t px = (size_t)r * W + line, off = px * D;
 #pragma unroll
             for (int i = 0; i < DPL; i++) c[i] = sd.cv[off + min(dbase + i, D - 1)];
-            bad = any_nonfinite<DPL>(c);
+            bad = any_nonfinite<DPL>(c, sd.pen[px * 16 + 2], sd.pen[px * 16 + 3]);
         }
         if (bad) {
             faithful_vertical<DPL>(sd.cv, sd.pen, sd.S, H, W, D, line, true, true, flds);

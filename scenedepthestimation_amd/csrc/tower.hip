@@ -1369,7 +1369,12 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     const float *w1 = packed;
     const float *wk = packed + L1_FLOATS + (int64_t)(layer - 2) * LK_FLOATS;
     const int hout = Hin - (layer == 2 ? 4 : 2), wout = Win - (layer == 2 ? 4 : 2);
-    if (f16 && layer >= 3 && !ohi && !onrm && (flags & SDE_TOWER_WINOGRAD)) {
+    // the Winograd kernel's input / output descriptors span a whole image with 32-bit record
+    // counts and offsets (tower_wino.h): planes of 4 GiB or more take the direct kernel, which
+    // rebases its descriptors per tile (same f16x3 arithmetic, fp32-level error either way)
+    const bool wino_fits = (int64_t)Hin * Win * 256 < ((int64_t)1 << 32) &&
+                           (int64_t)hout * wout * 256 < ((int64_t)1 << 32);
+    if (f16 && layer >= 3 && !ohi && !onrm && (flags & SDE_TOWER_WINOGRAD) && wino_fits) {
         // Winograd F(2x2, 3x3) for the 64 -> 64 layers (tower_wino.h)
         XpBatch bt;
         bt.tiles_x = cdiv(wout, WN_TX);

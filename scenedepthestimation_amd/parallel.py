@@ -13,6 +13,9 @@ The reference has no parallelism; two schemes a
   (strict `<` in rank order == lowest d on ties), so the result is bit-identical
   to WTA1(compute_cost_volume(...)) on one device.
 
+* disparity-sharded with the tower replicated (``ReplicatedDisparityShardedMatcher``): every
+  rank runs the whole tower, its disparity block of the fused CV + first-min, and the ONE
+  all-gather of the 8-byte partials -- no feature exchange.
 * row-band split (config 5's zero-exchange alternative, ``RowBandMatcher``):
   rank r owns image rows ``row_band(H, N, r)`` and computes the tower on them
   (+ halo; bound words all-reduced, 4 B per layer) and the fused cost volume +
@@ -21,7 +24,8 @@ The reference has no parallelism; two schemes a
   disparity rows assembles the map.  Same bits as one device.
 
 The collectives are plain torch.distributed calls, so the same code runs on
-gloo (CPU tests) and nccl (= RCCL on ROCm).
+gloo (CPU tests; device tensors staged through host memory, which is how the one-GPU
+multi-process tests run the real classes) and nccl (= RCCL on ROCm).
 """
 from __future__ import annotations
 
@@ -70,6 +74,23 @@ def init_from_env(backend: str | None = None):
     return rank, world, local
 
 
+def _host_staged(t: torch.Tensor, group=None) -> bool:
+    """gloo collectives take host tensors: device tensors are staged through host memory (the CPU
+    tests and the one-GPU multi-process tests); nccl (= RCCL) takes them as they are."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
+    """dist.all_gather_into_tensor, host-staged on gloo."""
+    if _host_staged(inp, group):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    return out
+
+
 def gather_partials(min_local: torch.Tensor, arg_local: torch.Tensor, world: int, group=None):
     """One all-gather of the per-pixel (min f32, argmin i32) partials -> ([N,H,W] f32, [N,H,W] i32)."""
     shape = tuple(min_local.shape)
@@ -78,7 +99,7 @@ def gather_partials(min_local: torch.Tensor, arg_local: torch.Tensor, world: int
     packed[0] = min_local.reshape(-1).view(torch.int32)
     packed[1] = arg_local.reshape(-1)
     out = torch.empty((world * 2, npix), dtype=torch.int32, device=min_local.device)   # concatenated form
-    dist.all_gather_into_tensor(out, packed, group=group)
+    all_gather_into(out, packed, group)
     out = out.view(world, 2, npix)
     mins = out[:, 0].contiguous().view(torch.float32).reshape((world,) + shape)
     args = out[:, 1].contiguous().reshape((world,) + shape)
@@ -87,13 +108,17 @@ def gather_partials(min_local: torch.Tensor, arg_local: torch.Tensor, world: int
 
 def gather_row_bands(band: torch.Tensor, full: torch.Tensor, world: int, group=None):
     """All-gather equal-height row bands [rpb, ...] into full [world*rpb, ...]."""
-    dist.all_gather_into_tensor(full, band, group=group)
-    return full
+    return all_gather_into(full, band, group)
 
 
 def allreduce_max_(words: torch.Tensor, group=None):
     """In-place MAX all-reduce of the f16x3 bound words (non-negative floats)."""
-    dist.all_reduce(words, op=dist.ReduceOp.MAX, group=group)
+    if _host_staged(words, group):
+        w = words.cpu()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX, group=group)
+        words.copy_(w)
+    else:
+        dist.all_reduce(words, op=dist.ReduceOp.MAX, group=group)
     return words
 
 
@@ -149,7 +174,7 @@ class DisparityShardedMatcher:
             words = torch.zeros((2, 64), dtype=torch.float32, device=m.device)
             for _ in range(L - 1):
                 allreduce_max_(words, self.group)
-        dist.all_gather_into_tensor(self.full, self.band, group=self.group)
+        all_gather_into(self.full, self.band, self.group)
         full = self.full.view(self.world, 2, self.rpb, self.W, m.nf)
         for i in range(2):
             m.feat[i].copy_(full[:, i].reshape(self.world * self.rpb, self.W, m.nf)[:self.H])
@@ -164,15 +189,63 @@ class DisparityShardedMatcher:
         return ops.argmin_merge(mins, args, out=self.disp)
 
 
+class ReplicatedDisparityShardedMatcher:
+    """Config 5 with the tower replicated: every rank runs the whole tower (no feature exchange),
+    the fused CV + first-min over its disparity block, and exactly ONE collective -- the
+    all-gather of the 8-byte (min, argmin) partials before the ordered merge (north_star's
+    scheme).  Per rank at 3840 x 2160, D = 512, N = 8: the full pair tower (~7 ms), a 64-disparity
+    shard (~1 ms) and 66 MB of partials out, against the band tower's 3.7 GB feature all-gather
+    (DESIGN.md sec. 6).  Same bits as one device."""
+
+    def __init__(self, H, W, D, rank, world, weights=None, nlayers=5, nf=64, group=None, tower_precision="f16x3"):
+        from .pipeline import StereoMatcher
+        self.H, self.W, self.D = H, W, D
+        self.rank, self.world, self.group = rank, world, group
+        self.d_range = shard_range(D, world, rank)
+        self.m = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, d_range=self.d_range,
+                               tower_precision=tower_precision)
+        self.disp = torch.empty((H, W), dtype=torch.float32, device=self.m.device)
+
+    def load_images(self, left_u8, right_u8):
+        self.m.load_images(left_u8, right_u8)
+
+    def match(self):
+        from . import ops
+        self.m.features()
+        _, mn, am = self.m.cost_wta(want=("min", "argmin"))
+        mins, args = gather_partials(mn, am, self.world, self.group)
+        return ops.argmin_merge(mins, args, out=self.disp)
+
+
 def gather_disparity_rows(band: torch.Tensor, H: int, world: int, out: torch.Tensor | None = None, group=None):
     """All-gather equal-height [rpb, W] disparity row bands (the last band zero-padded) -> [H, W]."""
     rpb = band.shape[0]
     full = torch.empty((world * rpb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
-    dist.all_gather_into_tensor(full, band.contiguous(), group=group)
+    all_gather_into(full, band.contiguous(), group)
     if out is None:
         return full[:H]
     out.copy_(full[:H])
     return out
+
+
+class FullImages:
+    """The whole pair's u8 images and padded z-normalised images (what StereoMatcher.load_images /
+    preprocess hold), without the full-size feature, tower and cost-volume buffers a row band
+    never uses."""
+
+    def __init__(self, H, W, nlayers, tower_precision, device=None):
+        from . import ops
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.tower_precision = tower_precision
+        self.img_u82 = torch.empty((2, H, W), dtype=torch.uint8, device=self.device)
+        self.img_pad2 = torch.empty((2, H + 2 * nlayers, W + 2 * nlayers), dtype=torch.float32, device=self.device)
+        self.stats2 = torch.empty((2 * ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=self.device)
+
+    def load_images(self, left_u8, right_u8):
+        import numpy as np
+        for dst, src in zip(self.img_u82, (left_u8, right_u8)):
+            t = src if isinstance(src, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(src, np.uint8))
+            dst.copy_(t, non_blocking=False)
 
 
 class RowBandMatcher:
@@ -189,10 +262,10 @@ class RowBandMatcher:
         self.r0, self.r1, self.rpb = row_band(H, world, rank)
         self.hb = self.r1 - self.r0
         L = nlayers
-        # the full images live here (preprocess needs whole-image statistics); the band matcher
-        # holds the band's padded rows, features and workspaces
-        self.full = StereoMatcher(H, W, D, weights=weights, nlayers=nlayers, nf=nf, tower_precision=tower_precision,
-                                  cv_mode=cv_mode)
+        # the full images and their padded z-normalised copies live here (preprocess needs
+        # whole-image statistics) -- nothing else at full size; the band matcher holds the band's
+        # padded rows, features and workspaces
+        self.full = FullImages(H, W, nlayers, tower_precision)
         self.band = StereoMatcher(max(self.hb, 1), W, D, weights=weights, nlayers=nlayers, nf=nf,
                                   tower_precision=tower_precision, cv_mode=cv_mode) if self.hb > 0 else None
         dev = self.full.device

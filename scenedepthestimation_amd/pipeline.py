@@ -27,8 +27,9 @@ AMAX_WORDS = 64   # f16x3 bound words per image in the tower workspace (TOWER_AM
 
 def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3", nf: int = 64, on_launch=None):
     """sde_tower_forward_batch's launch sequence (mc_cnn_brunch.py:31-48), one layer at a time, as a
-    generator: the same workspace layout, bound-word memset, image absmax and per-layer launches,
-    so the features are bit-identical to ops.tower_forward_batch.  It yields (stage, words) after the
+    generator: the same launches, bound-word memset and image absmax (each image's activations
+    packed at its layer's own size rather than the C path's fixed act_stride), so the features are
+    bit-identical to ops.tower_forward_batch.  It yields (stage, words) after the
     image bound (stage 1) and after every layer l < nlayers (stage l): the points at which a caller
     may combine the f16x3 bound words of row bands (all-reduce MAX, parallel.py) before the next
     layer reads them.  on_launch(layer, launch): optional wrapper around each layer's launch (timing).
@@ -148,7 +149,10 @@ class StereoMatcher:
 
     def features_from_padded(self, on_launch=None):
         """Tower only, on already-normalised padded images in self.img_pad (the pair per launch)."""
-        if on_launch is not None and not self.split:
+        if on_launch is not None and self.split:
+            raise ValueError("on_launch needs the layer-by-layer tower, which does not emit split planes "
+                             "(emit_split=True): time the one-call tower instead")
+        if on_launch is not None:
             run_tower(self.img_pad2, self.packed, self.nlayers, self.feat2, self.ws, self.tower_precision, self.nf,
                       on_launch=on_launch)
             self.split_valid = False

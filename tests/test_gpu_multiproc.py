@@ -1,0 +1,49 @@
+"""GPU: the product's multi-rank classes (parallel.py) at world 2 and 3 on the one GPU of the box.
+
+Each rank is a fresh child process (subprocess: no exec of this process) on cuda:0 with the gloo
+backend -- device tensors staged through host memory (parallel.all_gather_into / allreduce_max_);
+on an 8-GPU node the same code runs one rank per GPU over RCCL.  Covers the band tower's bound-
+word all-reduces, the feature all-gather, the partials all-gather + ordered merge, the replicated
+-tower scheme's single all-gather, and the row-band gather, including an empty trailing band
+(H = 3, world 3).  Every map must equal the single-device StereoMatcher's bit for bit."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,H,W,D", [(2, 70, 96, 64), (3, 40, 130, 96), (3, 3, 80, 32)])
+def test_multirank_classes_on_one_gpu(gpu, world, H, W, D):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), str(H), str(W),
+                                       str(D)], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        print(out)
+        assert p.returncode == 0, f"rank {r} failed:\n{out[-3000:]}"

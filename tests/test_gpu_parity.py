@@ -272,6 +272,29 @@ def test_tower_layer_api_matches_forward(gpu):
         assert torch.equal(x, full), (prec, cbl)
 
 
+def test_tower_winograd_large_plane_takes_direct_kernel(gpu):
+    """A 64->64 layer whose activation plane is >= 4 GiB (4100 x 4100 x 64 f32): the Winograd
+    kernel's 32-bit descriptors cannot span it, so f16x3w must run the direct f16x3 kernel --
+    bit-identical to precision "f16x3" (the wrapped record counts dropped stores)."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    L, Hin, Win = 5, 4100, 4100
+    assert Hin * Win * 256 >= 2 ** 32
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=4), L)))
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.rand((Hin, Win, 64), device="cuda", generator=g)
+    word = x.abs().max().reshape(1)
+    outs = []
+    for prec in ("f16x3", "f16x3w"):
+        y = torch.empty((Hin - 2, Win - 2, 64), device="cuda")
+        ob = torch.zeros(1, device="cuda")
+        ops.tower_layer(x, packed, L, 3, y, precision=prec, in_absmax=word, out_absmax=ob)
+        outs.append((y, ob))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    del x, outs
+    torch.cuda.empty_cache()
+
+
 def test_preprocess_u8(gpu, oracle):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(8)

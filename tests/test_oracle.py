@@ -36,6 +36,19 @@ def test_golden_wta1_and_fused_shards(oracle, golden, golden_cases):
         assert np.array_equal(arg.astype(np.float32), ref), n
 
 
+def test_golden_numpy_restatement(golden, golden_cases):
+    """The NumPy restatement bench.py times as a CPU baseline (oracle/np_restatement.py: the
+    reference's own np.multiply / np.sum / argmin expressions) reproduces every golden vector."""
+    from oracle.np_restatement import compute_cost_volume_np, wta1_np
+    for n in golden_cases:
+        fl, fr, d = golden[n + "__fl"], golden[n + "__fr"], int(golden[n + "__ndisp"])
+        cv = compute_cost_volume_np(fl, fr, d)
+        assert cv.tobytes() == golden[n + "__cv"].tobytes(), n
+        if np.isnan(cv).any():
+            continue
+        assert np.array_equal(wta1_np(cv), golden[n + "__disp"]), n
+
+
 def test_golden_wta_hwd_and_ties(oracle, golden):
     assert np.array_equal(oracle.WTA(golden["wta_hwd__vol"]), golden["wta_hwd__disp"])
     assert np.array_equal(oracle.WTA1(golden["wta_dhw__vol"]), golden["wta_dhw__disp"])
