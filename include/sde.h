@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SDE_ABI_VERSION 1
+#define SDE_ABI_VERSION 2
 
 typedef enum {
     SDE_OK = 0,
@@ -230,16 +230,18 @@ int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream);
 /*
  * Preprocess on device (match_single.py:34-43 + process_functional.py:13-19):
  * u8 image -> (I - mean) / std (population std, float32) written into the
- * interior of the zero-padded buffer out_pad [(H+2*pad)][(W+2*pad)].
- * scratch: SDE_PREPROCESS_SCRATCH_BYTES of device memory (exact integer pixel
- * sums; zeroed by the call on the stream).
+ * interior of the zero-padded buffer out_pad [(H+2*pad)][(W+2*pad)] -- bit for bit
+ * NumPy's np.mean / np.std over axes (0, 1) of the float32 image (its pairwise
+ * float32 reduction order) and the float32 elementwise expression.
+ * scratch: sde_preprocess_scratch_bytes(H, W) of device memory per image (the
+ * statistics and NumPy's per-8192-element partial sums; no initialisation needed).
  */
-#define SDE_PREPROCESS_SCRATCH_BYTES 16
+int64_t sde_preprocess_scratch_bytes(int H, int W);
 int sde_preprocess_u8(const uint8_t *img, int H, int W, int pad, float *out_pad, void *scratch,
                       void *stream);
 
-/* sde_preprocess_u8 over nimg images in one pair of launches: imgs [nimg][H][W],
- * out_pad [nimg][H+2*pad][W+2*pad], scratch nimg * SDE_PREPROCESS_SCRATCH_BYTES. */
+/* sde_preprocess_u8 over nimg images per launch: imgs [nimg][H][W], out_pad
+ * [nimg][H+2*pad][W+2*pad], scratch nimg * sde_preprocess_scratch_bytes(H, W). */
 int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int W, int pad, float *out_pad, void *scratch,
                             void *stream);
 

@@ -65,6 +65,7 @@ SIGNATURES = {
     "sde_absmax_f32_batch": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p]),
     "sde_preprocess_u8_batch": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "sde_preprocess_scratch_bytes": (c_int64, [c_int, c_int]),
     "sde_sgm_penalties": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_int64, c_double, c_void_p,
                                   c_void_p]),
     "sde_sgm_8path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

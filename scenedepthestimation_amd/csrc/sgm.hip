@@ -333,6 +333,29 @@ __device__ __forceinline__ int wta_pixel(const float (&o)[DPL], int dbase, int D
     return (arg == 0x7fffffff || v0 != v0) ? 0 : arg;
 }
 
+// The end of one step's 64-way merge in the fused WTA: the G lanes of the step (a DPP row group)
+// hold the merges of their PF partials each; quad_perm, quad_perm, row_half_mirror (and
+// row_mirror for G = 16) leave every lane with the G-lane result -- the merge is a total order
+// (first-min with index tie-break, no NaN partials), so any order agrees -- and lane q = 0 stores
+// the disparity (rule of WTA_and_SupixelRefinement_kernel: "no winner" -> 0) unless px < 0.
+template <int G>
+__device__ __forceinline__ void wta_block_store(float bv, int ba, int px, int q, float *disp)
+{
+    static_assert(G == 8 || G == 16, "the fused WTA merge reduces 8 or 16 lanes per step");
+#define SDE_WTA_DPP(CTRL)                                                           \
+    {                                                                               \
+        const float v2 = __int_as_float(dpp_i32<CTRL>(__float_as_int(bv)));         \
+        const int a2 = dpp_i32<CTRL>(ba);                                           \
+        wta_merge(bv, ba, v2, a2);                                                  \
+    }
+    SDE_WTA_DPP(0xB1)       // quad_perm [1,0,3,2]
+    SDE_WTA_DPP(0x4E)       // quad_perm [2,3,0,1]
+    SDE_WTA_DPP(0x141)      // row_half_mirror: the other quad of the 8
+    if (G == 16) SDE_WTA_DPP(0x140)     // row_mirror: the other 8 of the 16
+#undef SDE_WTA_DPP
+    if (q == 0 && px >= 0) disp[px] = (float)(ba == 0x7fffffff ? 0 : ba);
+}
+
 template <int DPL>
 struct Slot {
     float c[DPL];
@@ -448,10 +471,21 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     const int lane = threadIdx.x & 63;      // one wave per block: lane < 64 known to the compiler
     const int dbase = lane * DPL;
     const double INF = __builtin_inf();
-    // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block)
-    __shared__ float wbv[WTA ? PF * 64 : 1];
-    __shared__ int wba[WTA ? PF * 64 : 1];
-    __shared__ int wpx[WTA ? PF : 1];
+    // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block).
+    // G = 64 / PF lanes merge one step; lane l's partial of step j sits at j * WS + (l % PF) * G +
+    // l / PF with WS = 64 + G: the merge's reads (lane (st, q) takes partials q, q + G, .. of step
+    // st) then hit 32 distinct banks per half-wave and the per-step writes 2-way at most (free for
+    // ds_write_b32) -- the straight j * 64 + l layout made the merge reads 8-way conflicted (PMC:
+    // 65 % of the launch's LDS cycles were conflicts)
+    // The merge of a block of PF steps is spread over the next block's steps (one partial read and
+    // merge per step, the G-lane DPP reduction and the store at its last step), so the loop body
+    // stays one uniform step: a separate merge block after every PF steps made the compiler rotate
+    // the prefetch ring's registers at the loop back-edge and drain it (vmcnt(0) every PF steps).
+    // Partials and pixel indices are double-buffered by block parity.
+    constexpr int G = 64 / PF, WS = 64 + G;
+    __shared__ float wbv[WTA ? 2 * PF * WS : 1];
+    __shared__ int wba[WTA ? 2 * PF * WS : 1];
+    __shared__ int wpx[WTA ? 2 * PF : 1];
     __shared__ FaithLds<DPL> flds;
 
     if (DU && !FIRST) {
@@ -493,7 +527,13 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
 #pragma unroll
     for (int i = 0; i < DPL; i++) L[i] = 1.0;
 
+    // fused WTA: this lane's running merge over the previous block (lane (st, q) = (lane / G,
+    // lane % G) merges the partials of lanes PF q .. PF q + PF - 1 of step st of that block)
+    float mv_b = __builtin_inff();
+    int mv_a = 0x7fffffff;
+    const int wst = lane / G, wq = lane % G;
     for (int k0 = 0; k0 < g.n; k0 += PF) {
+        const int buf = (k0 / PF) & 1;              // this block's partial buffer; buf ^ 1 = the previous block's
 #pragma unroll
         for (int j = 0; j < PF; j++) {
             const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
@@ -548,9 +588,19 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 for (int i = 0; i < DPL; i++)
                     if (dbase + i < D && o[i] < bv) { bv = o[i]; ba = dbase + i; }
                 if (lane == 0 && o[0] != o[0]) { bv = -__builtin_inff(); ba = 0; }   // NaN S(0): d = 0
-                wbv[j * 64 + lane] = bv;
-                wba[j * 64 + lane] = ba;
-                if (lane == 0) wpx[j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+                const int slot = (buf * PF + j) * WS + (lane % PF) * G + lane / PF;
+                wbv[slot] = bv;
+                wba[slot] = ba;
+                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+                // one step of the previous block's merge (nothing to merge in the first block)
+                if (k0 > 0) {
+                    const int rs = ((buf ^ 1) * PF + wst) * WS + j * G + wq;
+                    const float v2 = wbv[rs];
+                    const int a2 = wba[rs];
+                    if (j == 0) { mv_b = v2; mv_a = a2; }
+                    else wta_merge(mv_b, mv_a, v2, a2);
+                    if (j == PF - 1) wta_block_store<G>(mv_b, mv_a, wpx[(buf ^ 1) * PF + wst], wq, sd.disp);
+                }
             } else if (k < g.n && keep && !(SGM_DIAG & 2)) {
                 if (VEC) {
                     if (dbase < D) {
@@ -584,30 +634,18 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
             ahead.advance(g);
         }
-        if (WTA) {
-            // the lanes read each other's LDS slots: make the cross-lane dependency explicit (one
-            // wave per workgroup, so a wave barrier orders the writes above before these reads)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // PF pixels x 64 lane partials: lane l merges lanes 8(l&7)..+7 of step l>>3 (increasing
-            // d), then the 8 octants of its step by xor-butterfly; the merge is a total order
-            // (first-min with index tie-break, no NaN partials), so any merge order agrees
-            constexpr int G = 64 / PF;      // lanes per step; each merges PF partials
-            const int st = lane / G, q = lane % G;
-            float bv = wbv[st * 64 + PF * q];
-            int ba = wba[st * 64 + PF * q];
+    }
+    if (WTA && g.n > 0) {
+        // the last block's merge (its partials are in buffer buf_last)
+        const int buf = ((g.n - 1) / PF) & 1;
+        float b = wbv[(buf * PF + wst) * WS + wq];
+        int ba = wba[(buf * PF + wst) * WS + wq];
 #pragma unroll
-            for (int t = 1; t < PF; t++) wta_merge(bv, ba, wbv[st * 64 + PF * q + t], wba[st * 64 + PF * q + t]);
-#pragma unroll
-            for (int o2 = 1; o2 < G; o2 <<= 1) wta_merge(bv, ba, __shfl_xor(bv, o2, 64), __shfl_xor(ba, o2, 64));
-            const int px = wpx[st];
-            if (q == 0 && px >= 0) sd.disp[px] = (float)(ba == 0x7fffffff ? 0 : ba);
-            // ... and these reads before the next block's writes to the same slots
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int t = 1; t < PF; t++) {
+            const int rs = (buf * PF + wst) * WS + t * G + wq;
+            wta_merge(b, ba, wbv[rs], wba[rs]);
         }
+        wta_block_store<G>(b, ba, wpx[buf * PF + wst], wq, sd.disp);
     }
     if (!DU && kf >= 0) {
         // the line again in the reference's exact arithmetic (no prefetch: rare path), storing from

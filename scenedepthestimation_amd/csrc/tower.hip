@@ -1076,81 +1076,142 @@ __global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict
     for (int n = 0; n < NF; n++) out[p * NF + n] = v[n] * inv;
 }
 
-// Per-image statistics: exact integer sum and sum of squares of the u8 pixels
-// (one 64-bit atomic pair per workgroup), finalised in double by every reader.
-__global__ __launch_bounds__(256) void image_sums_kernel(const uint8_t *__restrict__ img, int64_t n,
-                                                         unsigned long long *__restrict__ sums)
+// Per-image statistics exactly as NumPy computes them for match_single.py:40-41 (float32 image,
+// np.mean / np.std over axes (0, 1)): the reduction over both axes of a contiguous 2-D array adds,
+// from 0.0f in order, the pairwise sums (numpy pairwise_sum: blocks <= 128 with 8 accumulators,
+// larger blocks halved at a multiple of 8) of consecutive 8192-element pieces of the flattened
+// image (np.getbufsize()); mean = S / n in float32; std = sqrt(S' / n) with S' the same reduction
+// of (x - mean)^2 (float32 ops, no contraction: the library is built with -ffp-contract=off).
+// Pinned against NumPy in tests (test_preprocess_u8: bit-identical at every config size).
+// Scratch per image: [mean, std, -, -][one float per piece].
+constexpr int NP_PIECE = 8192;
+
+__device__ __forceinline__ float np_val(const uint8_t *img, int64_t i, float mean, bool sq)
 {
-    img += blockIdx.y * n;      // batch: image blockIdx.y, its two sums at sums[2 * blockIdx.y]
-    sums += 2 * blockIdx.y;
-    unsigned long long s = 0, q = 0;
-    // 16-B loads from the first 16-B boundary on; per load the 16 bytes' sum and sum of squares
-    // by v_dot4_u32_u8 (exact: at most 16 x 255^2 < 2^32), added into 64-bit totals
-    const int64_t head = std::min<int64_t>(n, (int64_t)((16 - ((uintptr_t)img & 15)) & 15));
-    const int64_t nv = (n - head) / 16;
-    const uint4 *v4 = reinterpret_cast<const uint4 *>(img + head);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
-        const uint4 w = v4[i];
-        unsigned ss = __builtin_amdgcn_udot4(w.x, 0x01010101u, 0u, false);
-        ss = __builtin_amdgcn_udot4(w.y, 0x01010101u, ss, false);
-        ss = __builtin_amdgcn_udot4(w.z, 0x01010101u, ss, false);
-        ss = __builtin_amdgcn_udot4(w.w, 0x01010101u, ss, false);
-        unsigned qq = __builtin_amdgcn_udot4(w.x, w.x, 0u, false);
-        qq = __builtin_amdgcn_udot4(w.y, w.y, qq, false);
-        qq = __builtin_amdgcn_udot4(w.z, w.z, qq, false);
-        qq = __builtin_amdgcn_udot4(w.w, w.w, qq, false);
-        s += ss;
-        q += qq;
+    const float x = (float)img[i];
+    if (!sq) return x;
+    const float d = x - mean;
+    return d * d;
+}
+
+// numpy pairwise_sum of a block of len <= 128 elements at s
+__device__ float np_leaf(const uint8_t *img, int64_t s, int len, float mean, bool sq)
+{
+    if (len < 8) {
+        float res = 0.0f;
+        for (int i = 0; i < len; i++) res += np_val(img, s + i, mean, sq);
+        return res;
     }
-    // the < 16 bytes before the boundary and the < 16 after the last full load: block 0's lanes 0-31
-    if (blockIdx.x == 0 && threadIdx.x < 32) {
-        const int64_t k = threadIdx.x < 16 ? (int64_t)threadIdx.x : head + nv * 16 + (threadIdx.x - 16);
-        if (threadIdx.x < 16 ? k < head : k < n) {
-            const unsigned v = img[k];
-            s += v;
-            q += v * v;
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = np_val(img, s + j, mean, sq);
+    int i = 8;
+    for (; i < len - (len % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) r[j] += np_val(img, s + i + j, mean, sq);
+    }
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < len; i++) res += np_val(img, s + i, mean, sq);
+    return res;
+}
+
+__device__ __forceinline__ int np_half(int len) { const int n2 = len / 2; return n2 - n2 % 8; }
+
+// One wave per 8192-element piece: its pairwise sum into the image's scratch.  A full piece is a
+// perfect tree of 64 blocks of 128 (lane l sums block l; the xor-butterfly adds adjacent subtrees,
+// and float addition is commutative); the last, short piece walks numpy's recursion: every lane
+// enumerates the blocks in order (lane k % 64 sums block k into LDS), lane 0 adds them up the tree.
+template <bool SQ>
+__global__ __launch_bounds__(64) void np_piece_kernel(const uint8_t *__restrict__ imgs, int64_t n, int sstride,
+                                                      float *__restrict__ scratch)
+{
+    const uint8_t *img = imgs + blockIdx.y * n;
+    float *st = scratch + (size_t)blockIdx.y * sstride;
+    const float mean = SQ ? st[0] : 0.0f;
+    const int lane = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * NP_PIECE;
+    const int m = (int)std::min<int64_t>(NP_PIECE, n - c0);
+    float sum;
+    if (m == NP_PIECE) {
+        sum = np_leaf(img, c0 + 128 * lane, 128, mean, SQ);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    } else {
+        __shared__ float leaf[256];
+        {
+            int ss[16], sl[16], sp = 0, k = 0;
+            ss[0] = 0; sl[0] = m;
+            while (sp >= 0) {
+                const int s0 = ss[sp], len = sl[sp];
+                sp--;
+                if (len <= 128) {
+                    if ((k & 63) == lane) leaf[k] = np_leaf(img, c0 + s0, len, mean, SQ);
+                    k++;
+                } else {
+                    const int n2 = np_half(len);
+                    ss[++sp] = s0 + n2; sl[sp] = len - n2;     // right, visited second
+                    ss[++sp] = s0; sl[sp] = n2;                // left first
+                }
+            }
+        }
+        __syncthreads();
+        sum = 0.0f;
+        if (lane == 0) {
+            // post-order evaluation of the same tree over the block sums
+            int fl[16], fs[16], sp = 0, k = 0;
+            float fv[16], ret = 0.0f;
+            fl[0] = m; fs[0] = 0;
+            while (sp >= 0) {
+                const int len = fl[sp];
+                if (len <= 128) {
+                    ret = leaf[k++];
+                    sp--;
+                } else if (fs[sp] == 0) {
+                    fs[sp] = 1;
+                    ++sp; fl[sp] = np_half(len); fs[sp] = 0;
+                    continue;
+                } else if (fs[sp] == 1) {
+                    fv[sp] = ret;
+                    fs[sp] = 2;
+                    const int n2 = np_half(len);
+                    ++sp; fl[sp] = len - n2; fs[sp] = 0;
+                    continue;
+                } else {
+                    ret = fv[sp] + ret;
+                    sp--;
+                }
+                // deliver ret to the parent frame (handled at its next visit)
+            }
+            sum = ret;
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s += __shfl_xor(s, o, 64);
-        q += __shfl_xor(q, o, 64);
-    }
-    __shared__ unsigned long long red[2][4];
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][wave] = s; red[1][wave] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long ts = 0, tq = 0;
-        for (int w = 0; w < 4; w++) { ts += red[0][w]; tq += red[1][w]; }
-        atomicAdd(&sums[0], ts);
-        atomicAdd(&sums[1], tq);
-    }
+    if (lane == 0) st[4 + blockIdx.x] = sum;
+}
+
+// S = 0.0f + piece 0 + piece 1 + ... in order; STAGE 0: mean = S / n, 1: std = sqrt(S / n)
+template <int STAGE>
+__global__ __launch_bounds__(64) void np_stat_kernel(float *__restrict__ scratch, int sstride, int npieces, int64_t n)
+{
+    if (threadIdx.x != 0) return;
+    float *st = scratch + (size_t)blockIdx.x * sstride;
+    float S = 0.0f;
+    for (int c = 0; c < npieces; c++) S += st[4 + c];
+    const float q = S / (float)n;
+    st[STAGE] = STAGE == 0 ? q : sqrtf(q);
 }
 
 // (I - mean) / std in float32 (match_single.py:40-41), zero border (process_functional.py:13-19).
 __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restrict__ img, int H, int W, int pad,
-                                                        const unsigned long long *__restrict__ sums,
+                                                        const float *__restrict__ scratch, int sstride,
                                                         float *__restrict__ out)
 {
     const int Wp = W + 2 * pad;
     img += (size_t)blockIdx.y * H * W;      // batch: image blockIdx.y
-    sums += 2 * blockIdx.y;
+    const float *st = scratch + (size_t)blockIdx.y * sstride;
     out += (size_t)blockIdx.y * (H + 2 * pad) * Wp;
-    // mean and std once per workgroup (the same double expressions: same bits), not per pixel
-    __shared__ float ms[2];
-    if (threadIdx.x == 0) {
-        const double n = (double)H * W;
-        const double mean_d = (double)sums[0] / n;
-        const double var_d = fmax((double)sums[1] / n - mean_d * mean_d, 0.0);
-        ms[0] = (float)mean_d;
-        ms[1] = (float)sqrt(var_d);
-    }
-    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)(H + 2 * pad) * Wp) return;
-    const float mean = ms[0], stdv = ms[1];
+    const float mean = st[0], stdv = st[1];
     // the padded image has < 2^31 pixels (checked by sde_preprocess_u8_batch)
     const int ii = (int)i;
     const int y = ii / Wp - pad, x = ii % Wp - pad;
@@ -1585,20 +1646,29 @@ SDE_EXPORT int sde_tower_forward(const float *img_pad, int H, int W, const float
                                    feat_hi, feat_lo, feat_norm, stream);
 }
 
+SDE_EXPORT int64_t sde_preprocess_scratch_bytes(int H, int W)
+{
+    if (H <= 0 || W <= 0) return -1;
+    const int64_t pieces = ((int64_t)H * W + NP_PIECE - 1) / NP_PIECE;
+    return ((4 + pieces) * 4 + 255) / 256 * 256;
+}
+
 SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int W, int pad, float *out_pad,
                                        void *scratch, void *stream)
 {
     if (!imgs || !out_pad || !scratch || nimg <= 0 || nimg > 65535 || H <= 0 || W <= 0 || pad < 0) return SDE_ERR_ARG;
-    hipStream_t st = as_stream(stream);
-    unsigned long long *sums = reinterpret_cast<unsigned long long *>(scratch);
-    if (hipMemsetAsync(sums, 0, (size_t)nimg * 2 * sizeof(unsigned long long), st) != hipSuccess)
-        return SDE_ERR_LAUNCH;
-    const int64_t npix = (int64_t)H * W;
-    const int blocks = (int)std::min<int64_t>(256, std::max<int64_t>(1, cdiv(npix, 256 * 16 * 2)));
-    image_sums_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(imgs, npix, sums);
     const int64_t n = (int64_t)(H + 2 * pad) * (W + 2 * pad);
     if (n >= ((int64_t)1 << 31)) return SDE_ERR_ARG;       // znorm_pad_kernel's 32-bit pixel index
-    znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256), nimg), 256, 0, st>>>(imgs, H, W, pad, sums, out_pad);
+    hipStream_t st = as_stream(stream);
+    const int64_t npix = (int64_t)H * W;
+    const int pieces = (int)((npix + NP_PIECE - 1) / NP_PIECE);
+    const int sstride = (int)(sde_preprocess_scratch_bytes(H, W) / 4);
+    float *sc = reinterpret_cast<float *>(scratch);
+    np_piece_kernel<false><<<dim3(pieces, nimg), 64, 0, st>>>(imgs, npix, sstride, sc);
+    np_stat_kernel<0><<<nimg, 64, 0, st>>>(sc, sstride, pieces, npix);
+    np_piece_kernel<true><<<dim3(pieces, nimg), 64, 0, st>>>(imgs, npix, sstride, sc);
+    np_stat_kernel<1><<<nimg, 64, 0, st>>>(sc, sstride, pieces, npix);
+    znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256), nimg), 256, 0, st>>>(imgs, H, W, pad, sc, sstride, out_pad);
     return launch_status();
 }
 

@@ -375,35 +375,43 @@ def tower_layer_batch(inp, packed, nlayers: int, layer: int, out, nf: int = 64, 
     return out
 
 
-PREPROCESS_SCRATCH_BYTES = 16
+def preprocess_scratch_bytes(H: int, W: int) -> int:
+    """Device scratch one image's preprocess needs (sde_preprocess_scratch_bytes)."""
+    n = int(lib.sde_preprocess_scratch_bytes(int(H), int(W)))
+    if n < 0:
+        raise ValueError("invalid image shape")
+    return n
 
 
 def preprocess_u8(img_u8, pad: int, out=None, stats=None):
-    """u8 [H,W] -> zero-padded z-normalised f32 [H+2p, W+2p] on the device.
-    stats: optional uint8 scratch tensor of PREPROCESS_SCRATCH_BYTES bytes."""
+    """u8 [H,W] -> zero-padded z-normalised f32 [H+2p, W+2p] on the device, bit-identical to
+    NumPy's (I - np.mean(I)) / np.std(I) on the float32 image (match_single.py:40-41).
+    stats: optional uint8 scratch tensor of preprocess_scratch_bytes(H, W) bytes."""
     H, W = img_u8.shape
     pi = _need(img_u8, "image", dtype=torch.uint8)
+    nb = preprocess_scratch_bytes(H, W)
     if out is None:
         out = _empty((H + 2 * pad, W + 2 * pad), torch.float32, img_u8)
     if stats is None:
-        stats = _empty((PREPROCESS_SCRATCH_BYTES,), torch.uint8, img_u8)
+        stats = _empty((nb,), torch.uint8, img_u8)
     check(lib.sde_preprocess_u8(pi, H, W, pad, _need(out, "out_pad", shape=(H + 2 * pad, W + 2 * pad)),
-                                _need(stats, "scratch", dtype=torch.uint8, shape=(PREPROCESS_SCRATCH_BYTES,)),
+                                _need(stats, "scratch", dtype=torch.uint8, shape=(nb,)),
                                 _stream()), "sde_preprocess_u8")
     return out
 
 
 def preprocess_u8_batch(imgs_u8, pad: int, out=None, stats=None):
     """u8 [N,H,W] -> zero-padded z-normalised f32 [N, H+2p, W+2p], all images per launch.
-    stats: optional uint8 scratch tensor of N * PREPROCESS_SCRATCH_BYTES bytes."""
+    stats: optional uint8 scratch tensor of N * preprocess_scratch_bytes(H, W) bytes."""
     N, H, W = imgs_u8.shape
     pi = _need(imgs_u8, "images", dtype=torch.uint8)
+    nb = N * preprocess_scratch_bytes(H, W)
     if out is None:
         out = _empty((N, H + 2 * pad, W + 2 * pad), torch.float32, imgs_u8)
     if stats is None:
-        stats = _empty((N * PREPROCESS_SCRATCH_BYTES,), torch.uint8, imgs_u8)
+        stats = _empty((nb,), torch.uint8, imgs_u8)
     check(lib.sde_preprocess_u8_batch(pi, N, H, W, pad, _need(out, "out_pad", shape=(N, H + 2 * pad, W + 2 * pad)),
-                                      _need(stats, "scratch", dtype=torch.uint8, shape=(N * PREPROCESS_SCRATCH_BYTES,)),
+                                      _need(stats, "scratch", dtype=torch.uint8, shape=(nb,)),
                                       _stream()), "sde_preprocess_u8_batch")
     return out
 

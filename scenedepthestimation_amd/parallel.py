@@ -239,7 +239,7 @@ class FullImages:
         self.tower_precision = tower_precision
         self.img_u82 = torch.empty((2, H, W), dtype=torch.uint8, device=self.device)
         self.img_pad2 = torch.empty((2, H + 2 * nlayers, W + 2 * nlayers), dtype=torch.float32, device=self.device)
-        self.stats2 = torch.empty((2 * ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=self.device)
+        self.stats2 = torch.empty((2 * ops.preprocess_scratch_bytes(H, W),), dtype=torch.uint8, device=self.device)
 
     def load_images(self, left_u8, right_u8):
         import numpy as np

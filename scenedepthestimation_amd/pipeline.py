@@ -111,8 +111,8 @@ class StereoMatcher:
         # both images in one allocation: the tower runs the pair per launch (sde_tower_forward_batch)
         self.img_pad2 = torch.empty((2, H + 2 * L, W + 2 * L), dtype=torch.float32, device=dev)
         self.img_pad = [self.img_pad2[0], self.img_pad2[1]]
-        self.stats2 = torch.empty((2 * ops.PREPROCESS_SCRATCH_BYTES,), dtype=torch.uint8, device=dev)
-        n = ops.PREPROCESS_SCRATCH_BYTES
+        n = ops.preprocess_scratch_bytes(H, W)
+        self.stats2 = torch.empty((2 * n,), dtype=torch.uint8, device=dev)
         self.stats = [self.stats2[:n], self.stats2[n:]]
         self.feat2 = torch.empty((2, H, W, nf), dtype=torch.float32, device=dev)
         self.feat = [self.feat2[0], self.feat2[1]]

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_status_strings():
-    assert _lib.lib.sde_abi_version() == 1
+    assert _lib.lib.sde_abi_version() == 2
     assert _lib.lib.sde_status_string(0) == b"ok"
     assert _lib.lib.sde_status_string(-1) == b"invalid argument"
     assert _lib.lib.sde_status_string(-3) == b"workspace too small"
@@ -123,6 +123,9 @@ def test_argument_validation_without_gpu():
     assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace
     assert lib.sde_cv_wta_split(1, 1, N, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 1 << 20, N) == ERR
     assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
+    assert lib.sde_preprocess_scratch_bytes(0, 4) == -1
+    # [mean, std, -, -] + one float per 8192-pixel piece, rounded to 256 B
+    assert lib.sde_preprocess_scratch_bytes(1024, 1024) == 768 and lib.sde_preprocess_scratch_bytes(3, 5) == 256
     assert lib.sde_tower_packed_floats(0, 64) == -1
     assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 4, 8, 14, 1, N) == ERR                          # aliased buffers
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 4, 8, 33, 1, N) == ERR                          # L1 > 32

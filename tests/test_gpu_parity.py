@@ -295,13 +295,20 @@ def test_tower_winograd_large_plane_takes_direct_kernel(gpu):
     torch.cuda.empty_cache()
 
 
-def test_preprocess_u8(gpu, oracle):
+@pytest.mark.parametrize("H,W", [(37, 53), (1, 9), (7, 1), (375, 450), (1024, 1024), (2000, 3000), (1110, 1390)])
+def test_preprocess_u8(gpu, oracle, H, W):
+    """Device z-norm + pad == NumPy's (I - np.mean(I)) / np.std(I) on the float32 image
+    (match_single.py:40-41) bit for bit, at the configs' sizes: NumPy's float32 reduction order
+    (pairwise sums of 8192-element pieces, added in order) restated on the device."""
     from scenedepthestimation_amd import ops
-    rng = np.random.default_rng(8)
-    img = rng.integers(0, 256, (37, 53)).astype(np.uint8)
+    rng = np.random.default_rng(H * 7 + W)
+    img = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    if H * W > 64:
+        img[: H // 3] = (img[: H // 3] // 4 + 60).astype(np.uint8)     # not uniform: a skewed histogram
     out = host(ops.preprocess_u8(dev(img), 5))
     ref = oracle.pad_image(oracle.znorm(img.astype(np.float32)), 11)
-    assert np.abs(out - ref).max() < 1e-5
+    print(H, W, "max |device - numpy|", float(np.abs(out - ref).max()))
+    assert out.tobytes() == ref.tobytes()
 
 
 # ----------------------------------------------------------------------------
