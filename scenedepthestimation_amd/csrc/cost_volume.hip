@@ -754,20 +754,24 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
         }
     };
     // stores 8j .. 8j+7 of the 32 (16 L, 16 R runs), issued in the first four dot rows so they
-    // drain while the strip computes; rows outside the image are skipped
+    // drain while the strip computes.  A row outside the image gets soffset C3_SKIPOFF: with any
+    // voffset (<= 252, or CD_OOB for lanes past nd) the sum stays below 2^32 and past the records
+    // (4 W D < 2^31), so the range check drops it -- no branch per store.
+    constexpr uint32_t C3_SKIPOFF = 0x7fffffffu;
     auto emit_store = [&](int qp, int j) {
+        const int rowstep = 16 * D;                         // 4 rows of the volume, bytes
 #pragma unroll
         for (int n = 8 * j; n < 8 * j + 8 && n < 32; n++) {
             if (n < 16) {
                 const int x = qp + wave + 4 * n;
-                if (x < W)
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d,
-                                                          (x * D + dc) * 4, 0);
+                const uint32_t so = x < W ? (uint32_t)(((qp + wave) * D + dc) * 4 + n * rowstep) : C3_SKIPOFF;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d, so, 0);
             } else {
                 const int xr = qp - dc - 63 + 4 * (n - 16) + wave;
-                if (xr >= 0 && xr < W)
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d,
-                                                          (xr * D + dc) * 4, 0);
+                const uint32_t so = (uint32_t)xr < (uint32_t)W
+                                        ? (uint32_t)(((qp - dc - 63 + wave) * D + dc) * 4 + (n - 16) * rowstep)
+                                        : C3_SKIPOFF;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d, so, 0);
             }
         }
     };

@@ -308,6 +308,247 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 
 }
 
+// ---------------------------------------------------------------------------
+// Warp-specialised row sweep (cv_wta_row2_kernel) -- the default.
+//
+// In cv_wta_row_kernel all eight waves stage the window's new tiles (split, norms, ring writes)
+// and then all compute, in lock-step barrier phases around one 8-wave workgroup per CU (PMC:
+// waves parked 38 % of their cycles, MFMA pipe ~10 % busy).  Here the roles are split: waves
+// 0-3 compute (each owns 32 left pixels of a 128-pixel superstrip: left split, 12 MFMAs per
+// right tile of its band, the certificate -- the same arithmetic and bound as above), waves 4-7
+// stage: each admits one 32-pixel right tile per superstrip (fp32 loads issued a superstrip
+// ahead, split into the ring's hi / lo planes, the tile's max squared norm and non-finite flag
+// as whole-wave reductions, no atomics).  One barrier per superstrip: while the compute waves
+// read window k, the stagers write window k+1's four new tiles into the slots of the tiles
+// superstrip k-1 retired (ring = window + 4 tiles: 14 at D = 192, 112 KB).
+// ---------------------------------------------------------------------------
+constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
+constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
+
+// one stager lane's 8 units (pixel u >> 4, channels 4 (u & 15) ..) of right tile T: unit u = lane + 64 i
+__device__ __forceinline__ void r2_load(const float *__restrict__ frrow, int W, int T, int lane, float4 (&v)[8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = rw_load(frrow, W, T, lane + 64 * i);
+}
+
+// split a loaded tile into ring slot `slot`; its max squared pixel norm and non-finite flag
+__device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *tbad, int slot, int lane,
+                                         const float4 (&v)[8])
+{
+    unsigned mx = 0u;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int u = lane + 64 * i, px = u >> 4, q = u & 15;
+        _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
+        rw_split(v[i].x, h0, l0); rw_split(v[i].y, h1, l1); rw_split(v[i].z, h2, l2); rw_split(v[i].w, h3, l3);
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const h4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+        char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
+        *reinterpret_cast<uint2 *>(base) = __builtin_bit_cast(uint2, hv);
+        *reinterpret_cast<uint2 *>(base + 256 * 16) = __builtin_bit_cast(uint2, lv);
+        // the pixel's squared norm: its 16 lanes are one DPP row (same adds as rw_store)
+        float ss = v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
+        ss += rw_dpp<0xB1>(ss);
+        ss += rw_dpp<0x4E>(ss);
+        ss += rw_dpp<0x141>(ss);
+        ss += rw_dpp<0x140>(ss);
+        mx = max(mx, __float_as_uint(ss));          // non-negative: bit patterns order as unsigned
+        bad |= rw_nonfinite(v[i].x) || rw_nonfinite(v[i].y) || rw_nonfinite(v[i].z) || rw_nonfinite(v[i].w);
+    }
+    // whole-wave maximum (every lane holds its rows' pixel norms) and any-non-finite
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    const bool anybad = __ballot(bad) != 0;
+    if (lane == 0) {
+        tmax[slot] = mx;
+        tbad[slot] = anybad ? 1u : 0u;
+    }
+}
+
+template <bool WANT_MIN>
+__global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+                                                          int H, int W, int d0, int d1, int tlo0, int nw, int nt,
+                                                          float *__restrict__ out_min, int32_t *__restrict__ out_arg,
+                                                          float *__restrict__ out_disp, unsigned *__restrict__ counter,
+                                                          int32_t *__restrict__ list)
+{
+    extern __shared__ __attribute__((aligned(16))) uint4 rsm2[];
+    uint4 *ring = rsm2;                                             // [nt][2 planes][32 px][8 chunks]
+    unsigned *tmax = reinterpret_cast<unsigned *>(ring + nt * 512);  // [nt] max squared pixel norm (f32 bits)
+    unsigned *tbad = tmax + nt;                                     // [nt] any non-finite channel
+
+    const int y = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+    const float *flrow = fl + (size_t)y * W * 64;
+    const float *frrow = fr + (size_t)y * W * 64;
+    const size_t rowpix = (size_t)y * W;
+    const int nss = (W + R2_NX - 1) / R2_NX;
+    auto slot_of = [&](int T) { int r = T % nt; return r < 0 ? r + nt : r; };
+
+    if (wave >= 4) {
+        // ---------------- stagers ----------------
+        const int sw = wave - 4;
+        // window 0 (nw tiles, tile tlo0 + t by wave t % 4) and this wave's tile of window 1
+        constexpr int MAXP = 4;                       // nw <= 14: at most 4 prologue tiles per stager
+        float4 pv[MAXP][8];
+#pragma unroll
+        for (int i = 0; i < MAXP; i++)
+            if (sw + 4 * i < nw) r2_load(frrow, W, tlo0 + sw + 4 * i, lane, pv[i]);
+        float4 nv[8];
+        if (nss > 1) r2_load(frrow, W, tlo0 + nw + sw, lane, nv);
+#pragma unroll
+        for (int i = 0; i < MAXP; i++)
+            if (sw + 4 * i < nw) r2_store(ring, tmax, tbad, slot_of(tlo0 + sw + 4 * i), lane, pv[i]);
+        __syncthreads();
+        for (int k = 0; k < nss; k++) {
+            // window k+1's new tile (loaded a superstrip ago) into the slot superstrip k-1 retired,
+            // then the load of window k+2's
+            if (k + 1 < nss) {
+                const int T = tlo0 + R2_NEW * (k + 1) + nw - R2_NEW + sw;
+                r2_store(ring, tmax, tbad, slot_of(T), lane, nv);
+                if (k + 2 < nss) r2_load(frrow, W, T + R2_NEW, lane, nv);
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
+    // ---------------- compute waves ----------------
+    float4 lraw[8];
+    auto load_left = [&](int kk) {
+        const int xx = kk * R2_NX + RW_T * wave + j;
+        const float4 *src = reinterpret_cast<const float4 *>(flrow) + (size_t)(xx < W ? xx : 0) * 16 + 2 * h;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) { lraw[2 * s2] = src[4 * s2]; lraw[2 * s2 + 1] = src[4 * s2 + 1]; }
+    };
+    load_left(0);
+    __syncthreads();
+
+    for (int k = 0; k < nss; k++) {
+        const int tlo = tlo0 + R2_NEW * k;
+        const bool more = k + 1 < nss;
+        const int xb = k * R2_NX + RW_T * wave;
+        const int x = xb + j;
+        const bool xok = x < W;
+        float best = -__builtin_inff(), second = -__builtin_inff();
+        int arg = -1;
+        float nl = 0.0f;
+        unsigned nmax2 = 0u, wbad = 0u;
+        bool lbad = false;
+        if (xb < W) {          // wave-uniform
+            rw_f16x8 bh[4], bl[4];
+            float ssl = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) {
+                const float4 a = lraw[2 * s2], b = lraw[2 * s2 + 1];
+                const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    _Float16 hh, ll;
+                    rw_split(v8[e], hh, ll);
+                    bh[s2][e] = hh;
+                    bl[s2][e] = ll;
+                    ssl += v8[e] * v8[e];
+                    lbad |= rw_nonfinite(v8[e]);
+                }
+            }
+            ssl += __shfl_xor(ssl, 32, 64);
+            lbad |= __shfl_xor((int)lbad, 32, 64) != 0;
+            nl = sqrtf(ssl) * FX_NORM_UP;
+            if (more) load_left(k + 1);
+
+            float b1[4], b2[4];
+            int ag[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) { b1[t] = -__builtin_inff(); b2[t] = -__builtin_inff(); ag[t] = -1; }
+            const int Ta = (xb - d1 + 1 + RW_T * 4096) / RW_T - 4096;
+            const int Tb = (xb + 31 - d0 + RW_T * 4096) / RW_T - 4096;
+            const int T0 = max(Ta, tlo), T1 = min(Tb, tlo + nw - 1);
+            int slot = slot_of(T0);
+            for (int T = T0; T <= T1; T++, slot = (slot + 1 == nt) ? 0 : slot + 1) {
+                const int dt = xb - RW_T * T;
+                const int dlo = dt - 31, dhi = dt + 31;
+                if (dhi < d0 || dlo >= d1) continue;     // wave-uniform
+                nmax2 = max(nmax2, tmax[slot]);
+                wbad |= tbad[slot];
+                const uint4 *tp = ring + slot * 512;
+                fx_floatx16 acc = {0};
+                rw_f16x8 ah[4], al[4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    const int sl = fx_slot(j, 2 * s2 + h);
+                    ah[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
+                    al[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2], bh[s2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bl[s2], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bh[s2], acc, 0, 0, 0);
+                const int dl = dt + j - 4 * h;
+                if (dlo >= d0 && dhi < d1) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int t = r & 3;
+                        const int d = dl - ((r & 3) + 8 * (r >> 2));
+                        const float sc = acc[r];
+                        const bool gt = sc > b1[t];
+                        ag[t] = gt ? d : ag[t];
+                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                        b1[t] = fmaxf(b1[t], sc);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {
+                        const int t = r & 3;
+                        const int d = dl - ((r & 3) + 8 * (r >> 2));
+                        const float sc = (d >= d0 && d < d1) ? acc[r] : -__builtin_inff();
+                        const bool gt = sc > b1[t];
+                        ag[t] = gt ? d : ag[t];
+                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
+                        b1[t] = fmaxf(b1[t], sc);
+                    }
+                }
+            }
+            best = b1[0]; second = b2[0]; arg = ag[0];
+#pragma unroll
+            for (int t = 1; t < 4; t++) fx_merge(best, arg, second, b1[t], ag[t], b2[t]);
+            {
+                const float bb = __shfl_xor(best, 32, 64), ss2 = __shfl_xor(second, 32, 64);
+                const int aa = __shfl_xor(arg, 32, 64);
+                fx_merge(best, arg, second, bb, aa, ss2);
+            }
+        }
+        // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
+        // barrier per superstrip orders both directions
+        __syncthreads();
+        if (xb < W && h == 0 && xok) {
+            const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
+            const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
+            const size_t p = rowpix + x;
+            if (!lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX && (best - second) > 2.0f * eps && arg >= 0) {
+                if (WANT_MIN) {
+                    float cost = -0.0f;
+                    if (x - arg >= 0)
+                        cost = dot64_exact_global(reinterpret_cast<const float4 *>(flrow + (size_t)x * 64),
+                                                  reinterpret_cast<const float4 *>(frrow + (size_t)(x - arg) * 64));
+                    out_min[p] = cost;
+                }
+                if (out_arg) out_arg[p] = arg;
+                if (out_disp) out_disp[p] = (float)arg;
+            } else {
+                list[atomicAdd(counter, 1u)] = (int32_t)p;
+            }
+        }
+    }
+}
+
 // tiles spanned by a superstrip's window and the first one (superstrip 0), floor division
 static void row_window(int d0, int d1, int &tlo0, int &ntw)
 {
@@ -319,25 +560,60 @@ static void row_window(int d0, int d1, int &tlo0, int &ntw)
 
 static size_t row_smem(int ntw) { return (size_t)ntw * 512 * 16 + (size_t)ntw * 8; }
 
+// the warp-specialised kernel's window (128-pixel superstrips) and ring (window + 4 tiles)
+static void row2_window(int d0, int d1, int &tlo0, int &nw)
+{
+    auto fdiv = [](int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); };
+    tlo0 = fdiv(-(d1 - 1), RW_T);
+    nw = fdiv(R2_NX - 1 - d0, RW_T) - tlo0 + 1;
+}
+
+#ifndef CV_ROW2
+#define CV_ROW2 1     // 0: the lock-step cv_wta_row_kernel (A/B builds)
+#endif
+
+static bool row2_supported(int d0, int d1)
+{
+    int tlo0 = 0, nw = 0;
+    row2_window(d0, d1, tlo0, nw);
+    return CV_ROW2 && nw <= 14;           // prologue: <= 4 tiles per stager; ring <= 18 tiles
+}
+
 bool row_cert_supported(int d0, int d1)
 {
     int tlo0 = 0, ntw = 0;
     row_window(d0, d1, tlo0, ntw);
-    return ntw <= 18;
+    return ntw <= 18 || row2_supported(d0, d1);
 }
 
 void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int d1, float *out_min, int32_t *out_arg,
                      float *out_disp, unsigned *counter, int32_t *list, hipStream_t st)
 {
-    int tlo0 = 0, ntw = 0;
-    row_window(d0, d1, tlo0, ntw);
     static std::atomic<uint64_t> attr{0};
     once_per_device(attr, [] {
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  150 * 1024);
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  150 * 1024);
     });
+    if (row2_supported(d0, d1)) {
+        int tlo0 = 0, nw = 0;
+        row2_window(d0, d1, tlo0, nw);
+        const int nt = nw + R2_NEW;
+        if (out_min)
+            cv_wta_row2_kernel<true><<<H, 512, row_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt, out_min,
+                                                                   out_arg, out_disp, counter, list);
+        else
+            cv_wta_row2_kernel<false><<<H, 512, row_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt, nullptr,
+                                                                    out_arg, out_disp, counter, list);
+        return;
+    }
+    int tlo0 = 0, ntw = 0;
+    row_window(d0, d1, tlo0, ntw);
     if (out_min)
         cv_wta_row_kernel<true><<<H, 512, row_smem(ntw), st>>>(fl, fr, H, W, d0, d1, tlo0, ntw, out_min, out_arg,
                                                                out_disp, counter, list);

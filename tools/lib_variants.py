@@ -34,12 +34,19 @@ for so in sos:
     lib.sde_cost_volume.argtypes = [P, P, I, I, I, I, I, I, F, P, P, P]
     lib.sde_cbca_pair.argtypes = [P, P, P, P, P, P, I, I, I, I, I, P]
     lib.sde_sgm_8path_wta_pair.argtypes = [P] * 8 + [I, I, I, I, P]
+    lib.sde_cv_wta.argtypes = [P, P, I, I, I, I, I, P, P, P, I, P, ctypes.c_int64, P]
     libs.append((os.path.basename(so), lib))
 s = torch.cuda.current_stream().cuda_stream
 
 
+cvws = torch.empty(_lib.lib.sde_cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device="cuda")
+
+
 def run(lib, w):
-    if w == "cvlr":
+    if w == "cvwta":     # certified fused CV + WTA (north-star kernel) on the fp32 features
+        assert lib.sde_cv_wta(fl.data_ptr(), fr.data_ptr(), H, W, 64, 0, D, disp[0].data_ptr(), None, None,
+                              _lib.SDE_CV_CERTIFIED, cvws.data_ptr(), cvws.numel(), s) == 0
+    elif w == "cvlr":
         assert lib.sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
                                    vol[1].data_ptr(), s) == 0
     elif w == "cbca":
@@ -53,7 +60,7 @@ def run(lib, w):
 
 def outputs(w):
     torch.cuda.synchronize()
-    return [t.clone() for t in (vol[:2] if w != "sgm" else disp)]
+    return [t.clone() for t in (vol[:2] if w not in ("sgm", "cvwta") else disp[:1] if w == "cvwta" else disp)]
 
 
 for w in what:
