@@ -18,7 +18,7 @@ import sys
 
 KERNELS = {   # key -> (substring of the kernel name, sum over distinct names)
     "tower_conv64_layer": ("conv64_x6p_kernel<false, false, true, true, true>", False),
-    "cv_wta_row": ("cv_wta_row_kernel", False),
+    "cv_wta_row": ("cv_wta_row2_kernel<false>", False),
     "cvlr": ("cvlr3_kernel", False),
     "cbca_pair_iteration": ("cbca_scan_kernel", True),
     "sgm_pair": ("sgm_scan_kernel", True),
