@@ -35,6 +35,27 @@ __device__ __forceinline__ float dot64_exact_global(const float4 *__restrict__ a
     return -(0.0f + res);
 }
 
+// the same bits with at most two 32-byte steps of loads in flight (for kernels at tight VGPR budgets)
+__device__ __forceinline__ float dot64_exact_global_lean(const float4 *__restrict__ a, const float4 *__restrict__ b)
+{
+    float acc[8];
+    {
+        const float4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+        acc[0] = a0.x * b0.x; acc[1] = a0.y * b0.y; acc[2] = a0.z * b0.z; acc[3] = a0.w * b0.w;
+        acc[4] = a1.x * b1.x; acc[5] = a1.y * b1.y; acc[6] = a1.z * b1.z; acc[7] = a1.w * b1.w;
+    }
+#pragma unroll 1
+    for (int m = 1; m < 8; m++) {
+        const float4 a0 = a[2 * m], a1 = a[2 * m + 1], b0 = b[2 * m], b1 = b[2 * m + 1];
+        const float p[8] = {a0.x * b0.x, a0.y * b0.y, a0.z * b0.z, a0.w * b0.w,
+                            a1.x * b1.x, a1.y * b1.y, a1.z * b1.z, a1.w * b1.w};
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) acc[jj] = acc[jj] + p[jj];
+    }
+    const float res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    return -(0.0f + res);
+}
+
 __device__ __forceinline__ int fx_slot(int r, int c8) { return r * 8 + (c8 ^ ((r >> 1) & 7)); }
 
 __device__ __forceinline__ void fx_split(float x, __bf16 &h, __bf16 &l)

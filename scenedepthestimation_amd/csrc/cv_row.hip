@@ -322,6 +322,11 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // read window k, the stagers write window k+1's four new tiles into the slots of the tiles
 // superstrip k-1 retired (ring = window + 4 tiles: 14 at D = 192, 112 KB).
 // ---------------------------------------------------------------------------
+#ifndef CV_DIAG
+#define CV_DIAG 0     // timing-only builds (tools/cv_variants.py): 1 stagers skip the split + ring writes,
+                      // 8 and their loads; 2 compute waves skip the MFMAs + scores, 4 their ring reads,
+                      // 16 the left operand's split.  0 in the library.
+#endif
 constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
 constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
 
@@ -367,8 +372,15 @@ __device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *
     }
 }
 
-template <bool WANT_MIN>
-__global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+// SPLIT = 2 (A/B builds, -DCV_ROW_SPLIT=2): two compute waves per 32-pixel group, each sweeping half of the group's
+// right tiles (waves g and g + 4 sit on the same SIMD: two independent MFMA -> score chains per SIMD
+// where SPLIT = 1 has one), 8 compute + 4 stager waves = 768 threads.  The halves' (best, runner-up,
+// argmin, window norm, non-finite) partials meet through LDS after the superstrip's barrier and both
+// waves merge them the same way (fx_merge is symmetric: the maximum, its smallest index among equal
+// scores, and the second largest of the union -- exactly the SPLIT = 1 values), then each certifies
+// half of the group's pixels.
+template <bool WANT_MIN, int SPLIT>
+__global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
                                                           int H, int W, int d0, int d1, int tlo0, int nw, int nt,
                                                           float *__restrict__ out_min, int32_t *__restrict__ out_arg,
                                                           float *__restrict__ out_disp, unsigned *__restrict__ counter,
@@ -378,6 +390,12 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     uint4 *ring = rsm2;                                             // [nt][2 planes][32 px][8 chunks]
     unsigned *tmax = reinterpret_cast<unsigned *>(ring + nt * 512);  // [nt] max squared pixel norm (f32 bits)
     unsigned *tbad = tmax + nt;                                     // [nt] any non-finite channel
+    // SPLIT = 2: the halves' partials [parity of k][half][group][pixel]
+    float *pbest = reinterpret_cast<float *>(tbad + nt);
+    float *psec = pbest + 2 * SPLIT * 128;
+    int *parg = reinterpret_cast<int *>(psec + 2 * SPLIT * 128);
+    unsigned *pn2 = reinterpret_cast<unsigned *>(parg + 2 * SPLIT * 128);
+    unsigned *pwb = pn2 + 2 * SPLIT * 128;
 
     const int y = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -389,28 +407,38 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     const int nss = (W + R2_NX - 1) / R2_NX;
     auto slot_of = [&](int T) { int r = T % nt; return r < 0 ? r + nt : r; };
 
-    if (wave >= 4) {
+    if (wave >= 4 * SPLIT) {
         // ---------------- stagers ----------------
-        const int sw = wave - 4;
+        const int sw = wave - 4 * SPLIT;
         // window 0 (nw tiles, tile tlo0 + t by wave t % 4) and this wave's tile of window 1
-        constexpr int MAXP = 4;                       // nw <= 14: at most 4 prologue tiles per stager
-        float4 pv[MAXP][8];
-#pragma unroll
-        for (int i = 0; i < MAXP; i++)
-            if (sw + 4 * i < nw) r2_load(frrow, W, tlo0 + sw + 4 * i, lane, pv[i]);
+        // (nw <= 14: at most 4 prologue tiles per stager; SPLIT = 2 loads them in two batches of two
+        // -- all four in flight at once would need 128 VGPRs, more than a 768-thread workgroup has)
+        constexpr int PB = SPLIT == 1 ? 4 : 2;         // tiles per batch
         float4 nv[8];
-        if (nss > 1) r2_load(frrow, W, tlo0 + nw + sw, lane, nv);
 #pragma unroll
-        for (int i = 0; i < MAXP; i++)
-            if (sw + 4 * i < nw) r2_store(ring, tmax, tbad, slot_of(tlo0 + sw + 4 * i), lane, pv[i]);
+        for (int b = 0; b < 4 / PB; b++) {
+            float4 pv[PB][8];
+#pragma unroll
+            for (int i = 0; i < PB; i++)
+                if (sw + 4 * (PB * b + i) < nw) r2_load(frrow, W, tlo0 + sw + 4 * (PB * b + i), lane, pv[i]);
+            if (b == 4 / PB - 1 && nss > 1) r2_load(frrow, W, tlo0 + nw + sw, lane, nv);
+#pragma unroll
+            for (int i = 0; i < PB; i++)
+                if (sw + 4 * (PB * b + i) < nw) r2_store(ring, tmax, tbad, slot_of(tlo0 + sw + 4 * (PB * b + i)), lane, pv[i]);
+        }
         __syncthreads();
         for (int k = 0; k < nss; k++) {
             // window k+1's new tile (loaded a superstrip ago) into the slot superstrip k-1 retired,
             // then the load of window k+2's
             if (k + 1 < nss) {
                 const int T = tlo0 + R2_NEW * (k + 1) + nw - R2_NEW + sw;
-                r2_store(ring, tmax, tbad, slot_of(T), lane, nv);
-                if (k + 2 < nss) r2_load(frrow, W, T + R2_NEW, lane, nv);
+                if (CV_DIAG & 1) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) asm volatile("" ::"v"(nv[i].x), "v"(nv[i].y), "v"(nv[i].z), "v"(nv[i].w));
+                } else {
+                    r2_store(ring, tmax, tbad, slot_of(T), lane, nv);
+                }
+                if (k + 2 < nss && !(CV_DIAG & 8)) r2_load(frrow, W, T + R2_NEW, lane, nv);
             }
             __syncthreads();
         }
@@ -418,9 +446,10 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     }
 
     // ---------------- compute waves ----------------
+    const int grp = wave & 3, hf = wave >> 2;       // pixel group, half of its right tiles
     float4 lraw[8];
     auto load_left = [&](int kk) {
-        const int xx = kk * R2_NX + RW_T * wave + j;
+        const int xx = kk * R2_NX + RW_T * grp + j;
         const float4 *src = reinterpret_cast<const float4 *>(flrow) + (size_t)(xx < W ? xx : 0) * 16 + 2 * h;
 #pragma unroll
         for (int s2 = 0; s2 < 4; s2++) { lraw[2 * s2] = src[4 * s2]; lraw[2 * s2 + 1] = src[4 * s2 + 1]; }
@@ -431,7 +460,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     for (int k = 0; k < nss; k++) {
         const int tlo = tlo0 + R2_NEW * k;
         const bool more = k + 1 < nss;
-        const int xb = k * R2_NX + RW_T * wave;
+        const int xb = k * R2_NX + RW_T * grp;
         const int x = xb + j;
         const bool xok = x < W;
         float best = -__builtin_inff(), second = -__builtin_inff();
@@ -439,6 +468,8 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
         float nl = 0.0f;
         unsigned nmax2 = 0u, wbad = 0u;
         bool lbad = false;
+        const int pslot = ((k & 1) * SPLIT + hf) * 128 + 32 * grp + j;    // this wave's partial
+        const int oslot = ((k & 1) * SPLIT + (1 - hf)) * 128 + 32 * grp + j;   // the other half's
         if (xb < W) {          // wave-uniform
             rw_f16x8 bh[4], bl[4];
             float ssl = 0.0f;
@@ -449,7 +480,8 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     _Float16 hh, ll;
-                    rw_split(v8[e], hh, ll);
+                    if (CV_DIAG & 16) { hh = (_Float16)(float)e; ll = (_Float16)(float)s2; }
+                    else rw_split(v8[e], hh, ll);
                     bh[s2][e] = hh;
                     bl[s2][e] = ll;
                     ssl += v8[e] * v8[e];
@@ -467,7 +499,12 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
             for (int t = 0; t < 4; t++) { b1[t] = -__builtin_inff(); b2[t] = -__builtin_inff(); ag[t] = -1; }
             const int Ta = (xb - d1 + 1 + RW_T * 4096) / RW_T - 4096;
             const int Tb = (xb + 31 - d0 + RW_T * 4096) / RW_T - 4096;
-            const int T0 = max(Ta, tlo), T1 = min(Tb, tlo + nw - 1);
+            int T0 = max(Ta, tlo), T1 = min(Tb, tlo + nw - 1);
+            if (SPLIT == 2) {                          // half 0: the first ceil(n / 2) tiles, half 1 the rest
+                const int mid = T0 + (T1 - T0 + 2) / 2;
+                if (hf == 0) T1 = mid - 1;
+                else T0 = mid;
+            }
             int slot = slot_of(T0);
             for (int T = T0; T <= T1; T++, slot = (slot + 1 == nt) ? 0 : slot + 1) {
                 const int dt = xb - RW_T * T;
@@ -481,8 +518,19 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
 #pragma unroll
                 for (int s2 = 0; s2 < 4; s2++) {
                     const int sl = fx_slot(j, 2 * s2 + h);
-                    ah[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
-                    al[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
+                    if (CV_DIAG & 4) {
+                        ah[s2] = bh[s2] * (_Float16)(float)T;
+                        al[s2] = bl[s2];
+                    } else {
+                        ah[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
+                        al[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
+                    }
+                }
+                if (CV_DIAG & 2) {
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; s2++) asm volatile("" ::"v"(ah[s2]), "v"(al[s2]));
+                    nmax2 += (unsigned)T;
+                    continue;
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; s2++) {
@@ -524,11 +572,22 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 const int aa = __shfl_xor(arg, 32, 64);
                 fx_merge(best, arg, second, bb, aa, ss2);
             }
+            if (SPLIT == 2 && h == 0) {
+                pbest[pslot] = best; psec[pslot] = second; parg[pslot] = arg;
+                pn2[pslot] = nmax2; pwb[pslot] = wbad;
+            }
         }
         // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
-        // barrier per superstrip orders both directions
+        // barrier per superstrip orders both directions (and publishes the halves' partials, which
+        // alternate buffers by the parity of k: a half writes buffer k & 1 again only after the
+        // next barrier, which the other half passes after its read)
         __syncthreads();
-        if (xb < W && h == 0 && xok) {
+        if (SPLIT == 2 && xb < W) {
+            fx_merge(best, arg, second, pbest[oslot], parg[oslot], psec[oslot]);
+            nmax2 = max(nmax2, pn2[oslot]);
+            wbad |= pwb[oslot];
+        }
+        if (xb < W && h == 0 && xok && (SPLIT == 1 || (j >> 4) == hf)) {
             const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
             const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
             const size_t p = rowpix + x;
@@ -536,14 +595,14 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 if (WANT_MIN) {
                     float cost = -0.0f;
                     if (x - arg >= 0)
-                        cost = dot64_exact_global(reinterpret_cast<const float4 *>(flrow + (size_t)x * 64),
+                        cost = dot64_exact_global_lean(reinterpret_cast<const float4 *>(flrow + (size_t)x * 64),
                                                   reinterpret_cast<const float4 *>(frrow + (size_t)(x - arg) * 64));
                     out_min[p] = cost;
                 }
                 if (out_arg) out_arg[p] = arg;
                 if (out_disp) out_disp[p] = (float)arg;
             } else {
-                list[atomicAdd(counter, 1u)] = (int32_t)p;
+                if (!CV_DIAG) list[atomicAdd(counter, 1u)] = (int32_t)p;   // (diagnostic builds: no fix-ups)
             }
         }
     }
@@ -571,6 +630,14 @@ static void row2_window(int d0, int d1, int &tlo0, int &nw)
 #ifndef CV_ROW2
 #define CV_ROW2 1     // 0: the lock-step cv_wta_row_kernel (A/B builds)
 #endif
+#ifndef CV_ROW_SPLIT
+// compute waves per 32-pixel group of the warp-specialised kernel: 1, or 2 (measured no faster at
+// 1024^2 x 192: 0.255 vs 0.246 ms median, round-robin on one box -- the compute waves' MFMA -> score
+// chain is not what bounds the kernel)
+#define CV_ROW_SPLIT 1
+#endif
+// the halves' partials (5 words per pixel, two parities) after the ring and its per-tile words
+static size_t row2_smem(int nt) { return row_smem(nt) + (CV_ROW_SPLIT == 2 ? (size_t)5 * 2 * 2 * 128 * 4 : 0); }
 
 static bool row2_supported(int d0, int d1)
 {
@@ -590,26 +657,28 @@ void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int
                      float *out_disp, unsigned *counter, int32_t *list, hipStream_t st)
 {
     static std::atomic<uint64_t> attr{0};
+    constexpr int SPLIT = CV_ROW_SPLIT;
+    constexpr int NT2 = 256 + 256 * SPLIT;
     once_per_device(attr, [] {
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
-        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  150 * 1024);
-        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  150 * 1024);
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<true, SPLIT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<false, SPLIT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     });
     if (row2_supported(d0, d1)) {
         int tlo0 = 0, nw = 0;
         row2_window(d0, d1, tlo0, nw);
         const int nt = nw + R2_NEW;
         if (out_min)
-            cv_wta_row2_kernel<true><<<H, 512, row_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt, out_min,
-                                                                   out_arg, out_disp, counter, list);
+            cv_wta_row2_kernel<true, SPLIT><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
+                                                                          out_min, out_arg, out_disp, counter, list);
         else
-            cv_wta_row2_kernel<false><<<H, 512, row_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt, nullptr,
-                                                                    out_arg, out_disp, counter, list);
+            cv_wta_row2_kernel<false, SPLIT><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
+                                                                           nullptr, out_arg, out_disp, counter, list);
         return;
     }
     int tlo0 = 0, ntw = 0;

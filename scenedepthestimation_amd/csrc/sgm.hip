@@ -474,9 +474,11 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block).
     // G = 64 / PF lanes merge one step; lane l's partial of step j sits at j * WS + (l % PF) * G +
     // l / PF with WS = 64 + G: the merge's reads (lane (st, q) takes partials q, q + G, .. of step
-    // st) then hit 32 distinct banks per half-wave and the per-step writes 2-way at most (free for
-    // ds_write_b32) -- the straight j * 64 + l layout made the merge reads 8-way conflicted (PMC:
-    // 65 % of the launch's LDS cycles were conflicts)
+    // st) then hit 32 distinct banks per half-wave -- the straight j * 64 + l layout made the merge
+    // reads 8-way conflicted (PMC: 65 % of the launch's LDS cycles were conflicts).  Within a step's
+    // row, the G-word group of lane l % PF is XOR-swizzled by (l % PF) & 4: lanes l and l + 4 (same
+    // l / PF, rows 32 words apart in bank space) then land in disjoint halves of their 8 banks, so
+    // the per-step ds_write_b32s are conflict-free too (were 2-way: 28 % of the launch's LDS cycles)
     // The merge of a block of PF steps is spread over the next block's steps (one partial read and
     // merge per step, the G-lane DPP reduction and the store at its last step), so the loop body
     // stays one uniform step: a separate merge block after every PF steps made the compiler rotate
@@ -588,13 +590,13 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 for (int i = 0; i < DPL; i++)
                     if (dbase + i < D && o[i] < bv) { bv = o[i]; ba = dbase + i; }
                 if (lane == 0 && o[0] != o[0]) { bv = -__builtin_inff(); ba = 0; }   // NaN S(0): d = 0
-                const int slot = (buf * PF + j) * WS + (lane % PF) * G + lane / PF;
+                const int slot = (buf * PF + j) * WS + (lane % PF) * G + ((lane / PF) ^ (lane % PF & 4));
                 wbv[slot] = bv;
                 wba[slot] = ba;
                 if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
                 // one step of the previous block's merge (nothing to merge in the first block)
                 if (k0 > 0) {
-                    const int rs = ((buf ^ 1) * PF + wst) * WS + j * G + wq;
+                    const int rs = ((buf ^ 1) * PF + wst) * WS + j * G + (wq ^ (j & 4));
                     const float v2 = wbv[rs];
                     const int a2 = wba[rs];
                     if (j == 0) { mv_b = v2; mv_a = a2; }
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         int ba = wba[(buf * PF + wst) * WS + wq];
 #pragma unroll
         for (int t = 1; t < PF; t++) {
-            const int rs = (buf * PF + wst) * WS + t * G + wq;
+            const int rs = (buf * PF + wst) * WS + t * G + (wq ^ (t & 4));
             wta_merge(b, ba, wbv[rs], wba[rs]);
         }
         wta_block_store<G>(b, ba, wpx[buf * PF + wst], wq, sd.disp);
