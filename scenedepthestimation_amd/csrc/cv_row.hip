@@ -532,6 +532,14 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                     nmax2 += (unsigned)T;
                     continue;
                 }
+                if (CV_DIAG & 128) {     // no MFMAs: scores from the fragments' bits (operands kept live)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; s2++)
+#pragma unroll
+                        for (int e = 0; e < 4; e++)
+                            acc[4 * s2 + e] = (float)ah[s2][2 * e] + (float)al[s2][2 * e + 1] + (float)bh[s2][e] +
+                                              (float)bl[s2][e + 4];
+                } else {
 #pragma unroll
                 for (int s2 = 0; s2 < 4; s2++) {
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2], bh[s2], acc, 0, 0, 0);
@@ -539,15 +547,31 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bh[s2], acc, 0, 0, 0);
+                }
+                if (CV_DIAG & 64) {      // no scoring: the accumulators folded into one live value
+                    float z = 0.f;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) asm volatile("" ::"v"(acc[r]));
+                    b1[0] = fmaxf(b1[0], acc[0] + (float)T);
+                    continue;
+                }
+                // register r holds d = dl - t - 8k (t = r & 3, k = r >> 2); chain t keeps d + t = dk[k]
+                // (four adds per tile instead of sixteen) and subtracts t once at the end
                 const int dl = dt + j - 4 * h;
+                int dk[4];
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) dk[k2] = dl - 8 * k2;
                 if (dlo >= d0 && dhi < d1) {
+                    // (an opaque statement: keeps this path a real scalar branch -- merged with the edge
+                    // path below into selects, every interior tile paid the edge path's 31 range
+                    // compares and 16 masking selects)
+                    asm volatile("");
 #pragma unroll
                     for (int r = 0; r < 16; r++) {
                         const int t = r & 3;
-                        const int d = dl - ((r & 3) + 8 * (r >> 2));
                         const float sc = acc[r];
                         const bool gt = sc > b1[t];
-                        ag[t] = gt ? d : ag[t];
+                        if (!(CV_DIAG & 256)) ag[t] = gt ? dk[r >> 2] : ag[t];
                         b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
                         b1[t] = fmaxf(b1[t], sc);
                     }
@@ -555,15 +579,18 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
 #pragma unroll
                     for (int r = 0; r < 16; r++) {
                         const int t = r & 3;
-                        const int d = dl - ((r & 3) + 8 * (r >> 2));
+                        const int d = dk[r >> 2] - t;
                         const float sc = (d >= d0 && d < d1) ? acc[r] : -__builtin_inff();
                         const bool gt = sc > b1[t];
-                        ag[t] = gt ? d : ag[t];
+                        ag[t] = gt ? dk[r >> 2] : ag[t];
                         b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
                         b1[t] = fmaxf(b1[t], sc);
                     }
                 }
             }
+            // a chain that took a score holds d + t >= t >= 0; one that took none still holds -1
+#pragma unroll
+            for (int t = 0; t < 4; t++) ag[t] = ag[t] >= 0 ? ag[t] - t : -1;
             best = b1[0]; second = b2[0]; arg = ag[0];
 #pragma unroll
             for (int t = 1; t < 4; t++) fx_merge(best, arg, second, b1[t], ag[t], b2[t]);
