@@ -9,6 +9,7 @@
 #include "cv_cert.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace sde {
 
@@ -322,6 +323,9 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // read window k, the stagers write window k+1's four new tiles into the slots of the tiles
 // superstrip k-1 retired (ring = window + 4 tiles: 14 at D = 192, 112 KB).
 // ---------------------------------------------------------------------------
+#ifndef CV_PIPE
+#define CV_PIPE 1     // software-pipelined tile sweep in cv_wta_row2_kernel (0: the plain loop)
+#endif
 #ifndef CV_DIAG
 #define CV_DIAG 0     // timing-only builds (tools/cv_variants.py): 1 stagers skip the split + ring writes,
                       // 8 and their loads; 2 compute waves skip the MFMAs + scores, 4 their ring reads,
@@ -506,6 +510,101 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                 else T0 = mid;
             }
             int slot = slot_of(T0);
+#if CV_PIPE
+            if (CV_DIAG == 0) {
+                // software-pipelined sweep: tile i's 16 scores are interleaved with the 12 MFMAs of
+                // tile i + 1 (after two scores that cover the fragment reads' LDS latency: one MFMA,
+                // then the VALU of 1-2 scores, per gap -- the MFMA pipe runs while the scores issue).
+                // Same scores, same order of score updates: the same outputs.
+                // (every T in [T0, T1] is inside the band: Ta / Tb are its exact bounds)
+                const int n = T1 - T0 + 1;
+                rw_f16x8 fh[4], fo[4];
+                fx_floatx16 A[2];
+                auto nxt = [&](int sl2) { return sl2 + 1 == nt ? 0 : sl2 + 1; };
+                auto frag = [&](int sl2) {
+                    const uint4 *tp = ring + sl2 * 512;
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; s2++) {
+                        const int sl = fx_slot(j, 2 * s2 + h);
+                        fh[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
+                        fo[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
+                    }
+                };
+                // MFMA m (0..11) of a tile: the small terms first, then the leading products
+                auto mfma = [&](int m, fx_floatx16 &acc) {
+                    if (m == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fo[0], bh[0], fx_floatx16{0}, 0, 0, 0);
+                    else if (m < 8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((m & 1) ? fh[m >> 1] : fo[m >> 1],
+                                                                                (m & 1) ? bl[m >> 1] : bh[m >> 1],
+                                                                                acc, 0, 0, 0);
+                    else acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[m - 8], bh[m - 8], acc, 0, 0, 0);
+                };
+                auto score1 = [&](const fx_floatx16 &acc, int r, bool full, const int (&dk)[4]) {
+                    const int tt = r & 3;
+                    const float sc = full || ((dk[r >> 2] - tt) >= d0 && (dk[r >> 2] - tt) < d1) ? acc[r]
+                                                                                                 : -__builtin_inff();
+                    const bool gt = sc > b1[tt];
+                    ag[tt] = gt ? dk[r >> 2] : ag[tt];
+                    b2[tt] = __builtin_amdgcn_fmed3f(b1[tt], b2[tt], sc);
+                    b1[tt] = fmaxf(b1[tt], sc);
+                };
+                // scores of tile T (accumulators acc, ring slot sl2) interleaved with the MFMAs of the
+                // next tile (slot nsl) into accn
+                auto step = [&](auto issue_c, int T, int sl2, const fx_floatx16 &acc, int nsl, fx_floatx16 &accn) {
+                    constexpr bool issue = decltype(issue_c)::value;
+                    if (issue) frag(nsl);
+                    nmax2 = max(nmax2, tmax[sl2]);
+                    wbad |= tbad[sl2];
+                    const int dt = xb - RW_T * T;
+                    const bool full = dt - 31 >= d0 && dt + 31 < d1;      // wave-uniform
+                    const int dl = dt + j - 4 * h;
+                    int dk[4];
+#pragma unroll
+                    for (int k2 = 0; k2 < 4; k2++) dk[k2] = dl - 8 * k2;
+                    if (full) {
+                        asm volatile("");
+                        score1(acc, 0, true, dk);
+                        score1(acc, 1, true, dk);
+#pragma unroll
+                        for (int m = 0; m < 12; m++) {
+                            if (issue) mfma(m, accn);
+#pragma unroll
+                            for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, true, dk);
+                        }
+                    } else {
+                        score1(acc, 0, false, dk);
+                        score1(acc, 1, false, dk);
+#pragma unroll
+                        for (int m = 0; m < 12; m++) {
+                            if (issue) mfma(m, accn);
+#pragma unroll
+                            for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, false, dk);
+                        }
+                    }
+                };
+                if (n > 0) {
+                    int sa = slot;                              // slot of tile T0 + i2
+                    frag(sa);
+#pragma unroll
+                    for (int m = 0; m < 12; m++) mfma(m, A[0]);
+                    using yes = std::integral_constant<bool, true>;
+                    using no = std::integral_constant<bool, false>;
+                    int i2 = 0;
+                    for (; i2 + 2 < n; i2 += 2) {              // two tiles per trip: static accumulators
+                        const int sb = nxt(sa), sc2 = nxt(sb);
+                        step(yes{}, T0 + i2, sa, A[0], sb, A[1]);
+                        step(yes{}, T0 + i2 + 1, sb, A[1], sc2, A[0]);
+                        sa = sc2;
+                    }
+                    if (i2 + 1 < n) {                          // two tiles left
+                        const int sb = nxt(sa);
+                        step(yes{}, T0 + i2, sa, A[0], sb, A[1]);
+                        step(no{}, T0 + i2 + 1, sb, A[1], sb, A[0]);
+                    } else {                                   // one tile left
+                        step(no{}, T0 + i2, sa, A[0], sa, A[1]);
+                    }
+                }
+            } else
+#endif
             for (int T = T0; T <= T1; T++, slot = (slot + 1 == nt) ? 0 : slot + 1) {
                 const int dt = xb - RW_T * T;
                 const int dlo = dt - 31, dhi = dt + 31;

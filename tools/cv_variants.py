@@ -44,7 +44,7 @@ for name, lib in libs:
         ref = o
     print(f"cv: {name} disparities identical: {torch.equal(o[0], ref[0])}, fix-ups {o[1]}", flush=True)
 times = {n: [] for n, _ in libs}
-for rnd in range(5):
+for rnd in range(int(os.environ.get('CV_ROUNDS', '5'))):
     for name, lib in libs:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -54,4 +54,5 @@ for rnd in range(5):
         torch.cuda.synchronize()
         times[name].append(e0.elapsed_time(e1) / 5)
 for name, t in times.items():
-    print(f"cv  {name:22s} median {statistics.median(t):7.3f} ms  ({' '.join(f'{x:.3f}' for x in t)})", flush=True)
+    print(f"cv  {name:22s} median {statistics.median(t):7.3f} ms  min {min(t):7.3f}  ({' '.join(f'{x:.3f}' for x in t)})",
+          flush=True)
