@@ -518,25 +518,28 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                 // Same scores, same order of score updates: the same outputs.
                 // (every T in [T0, T1] is inside the band: Ta / Tb are its exact bounds)
                 const int n = T1 - T0 + 1;
-                rw_f16x8 fh[4], fo[4];
+                // PD = 2 (CV_PIPE 2): tile i + 2's fragments are read during tile i's step, a whole
+                // step before its MFMAs (two fragment buffers); PD = 1: at the start of the step
+                constexpr int PD = CV_PIPE >= 2 ? 2 : 1;
+                rw_f16x8 fh[PD][4], fo[PD][4];
                 fx_floatx16 A[2];
                 auto nxt = [&](int sl2) { return sl2 + 1 == nt ? 0 : sl2 + 1; };
-                auto frag = [&](int sl2) {
+                auto frag = [&](int sl2, rw_f16x8 (&ah)[4], rw_f16x8 (&al)[4]) {
                     const uint4 *tp = ring + sl2 * 512;
 #pragma unroll
                     for (int s2 = 0; s2 < 4; s2++) {
                         const int sl = fx_slot(j, 2 * s2 + h);
-                        fh[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
-                        fo[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
+                        ah[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
+                        al[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
                     }
                 };
                 // MFMA m (0..11) of a tile: the small terms first, then the leading products
-                auto mfma = [&](int m, fx_floatx16 &acc) {
-                    if (m == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fo[0], bh[0], fx_floatx16{0}, 0, 0, 0);
-                    else if (m < 8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((m & 1) ? fh[m >> 1] : fo[m >> 1],
+                auto mfma = [&](int m, fx_floatx16 &acc, const rw_f16x8 (&ah)[4], const rw_f16x8 (&al)[4]) {
+                    if (m == 0) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[0], bh[0], fx_floatx16{0}, 0, 0, 0);
+                    else if (m < 8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((m & 1) ? ah[m >> 1] : al[m >> 1],
                                                                                 (m & 1) ? bl[m >> 1] : bh[m >> 1],
                                                                                 acc, 0, 0, 0);
-                    else acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[m - 8], bh[m - 8], acc, 0, 0, 0);
+                    else acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m - 8], bh[m - 8], acc, 0, 0, 0);
                 };
                 auto score1 = [&](const fx_floatx16 &acc, int r, bool full, const int (&dk)[4]) {
                     const int tt = r & 3;
@@ -548,10 +551,14 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                     b1[tt] = fmaxf(b1[tt], sc);
                 };
                 // scores of tile T (accumulators acc, ring slot sl2) interleaved with the MFMAs of the
-                // next tile (slot nsl) into accn
-                auto step = [&](auto issue_c, int T, int sl2, const fx_floatx16 &acc, int nsl, fx_floatx16 &accn) {
-                    constexpr bool issue = decltype(issue_c)::value;
-                    if (issue) frag(nsl);
+                // next tile (slot nsl; fragments fb, read now when PD = 1) into accn; PD = 2: the
+                // fragments of the tile after it (slot lsl) are read into lb first
+                auto step = [&](auto issue_c, auto load_c, int T, int sl2, const fx_floatx16 &acc, int nsl,
+                                fx_floatx16 &accn, rw_f16x8 (&fbh)[4], rw_f16x8 (&fbl)[4], int lsl,
+                                rw_f16x8 (&lbh)[4], rw_f16x8 (&lbl)[4]) {
+                    constexpr bool issue = decltype(issue_c)::value, load = decltype(load_c)::value;
+                    if (PD == 1 && issue) frag(nsl, fbh, fbl);
+                    if (PD == 2 && load) frag(lsl, lbh, lbl);
                     nmax2 = max(nmax2, tmax[sl2]);
                     wbad |= tbad[sl2];
                     const int dt = xb - RW_T * T;
@@ -566,7 +573,7 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                         score1(acc, 1, true, dk);
 #pragma unroll
                         for (int m = 0; m < 12; m++) {
-                            if (issue) mfma(m, accn);
+                            if (issue) mfma(m, accn, fbh, fbl);
 #pragma unroll
                             for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, true, dk);
                         }
@@ -575,32 +582,39 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                         score1(acc, 1, false, dk);
 #pragma unroll
                         for (int m = 0; m < 12; m++) {
-                            if (issue) mfma(m, accn);
+                            if (issue) mfma(m, accn, fbh, fbl);
 #pragma unroll
                             for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, false, dk);
                         }
                     }
                 };
                 if (n > 0) {
-                    int sa = slot;                              // slot of tile T0 + i2
-                    frag(sa);
-#pragma unroll
-                    for (int m = 0; m < 12; m++) mfma(m, A[0]);
                     using yes = std::integral_constant<bool, true>;
                     using no = std::integral_constant<bool, false>;
+                    constexpr int B1 = PD - 1;                 // the buffer of odd tiles
+                    int sa = slot;                              // slot of tile T0 + i2
+                    frag(sa, fh[0], fo[0]);
+                    if (PD == 2 && n > 1) frag(nxt(sa), fh[B1], fo[B1]);
+#pragma unroll
+                    for (int m = 0; m < 12; m++) mfma(m, A[0], fh[0], fo[0]);
                     int i2 = 0;
-                    for (; i2 + 2 < n; i2 += 2) {              // two tiles per trip: static accumulators
-                        const int sb = nxt(sa), sc2 = nxt(sb);
-                        step(yes{}, T0 + i2, sa, A[0], sb, A[1]);
-                        step(yes{}, T0 + i2 + 1, sb, A[1], sc2, A[0]);
+                    for (; i2 + 3 < n; i2 += 2) {              // two tiles per trip: static buffers
+                        const int sb = nxt(sa), sc2 = nxt(sb), sd = nxt(sc2);
+                        step(yes{}, yes{}, T0 + i2, sa, A[0], sb, A[1], fh[B1], fo[B1], sc2, fh[0], fo[0]);
+                        step(yes{}, yes{}, T0 + i2 + 1, sb, A[1], sc2, A[0], fh[0], fo[0], sd, fh[B1], fo[B1]);
                         sa = sc2;
                     }
-                    if (i2 + 1 < n) {                          // two tiles left
-                        const int sb = nxt(sa);
-                        step(yes{}, T0 + i2, sa, A[0], sb, A[1]);
-                        step(no{}, T0 + i2 + 1, sb, A[1], sb, A[0]);
-                    } else {                                   // one tile left
-                        step(no{}, T0 + i2, sa, A[0], sa, A[1]);
+                    // the last 1-3 tiles
+                    const int sb = nxt(sa), sc2 = nxt(sb);
+                    if (i2 + 2 < n) {
+                        step(yes{}, yes{}, T0 + i2, sa, A[0], sb, A[1], fh[B1], fo[B1], sc2, fh[0], fo[0]);
+                        step(yes{}, no{}, T0 + i2 + 1, sb, A[1], sc2, A[0], fh[0], fo[0], sc2, fh[B1], fo[B1]);
+                        step(no{}, no{}, T0 + i2 + 2, sc2, A[0], sc2, A[1], fh[B1], fo[B1], sc2, fh[0], fo[0]);
+                    } else if (i2 + 1 < n) {
+                        step(yes{}, no{}, T0 + i2, sa, A[0], sb, A[1], fh[B1], fo[B1], sb, fh[0], fo[0]);
+                        step(no{}, no{}, T0 + i2 + 1, sb, A[1], sb, A[0], fh[0], fo[0], sb, fh[B1], fo[B1]);
+                    } else {
+                        step(no{}, no{}, T0 + i2, sa, A[0], sa, A[1], fh[B1], fo[B1], sa, fh[0], fo[0]);
                     }
                 }
             } else
