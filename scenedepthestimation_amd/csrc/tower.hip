@@ -1023,7 +1023,13 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
 }  // namespace sde
 #include "tower_wino.h"
+#include "tower_skew.h"
 namespace sde {
+
+#ifndef TOWER_SKEW
+#define TOWER_SKEW 0     // 1: f16x3 non-last layers on conv64_skew_kernel (tower_skew.h: bit-identical, measured
+                         // slower -- 248-254 vs 233 us per layer-image, tower pair 1.80-1.84 vs 1.74-1.75 ms)
+#endif
 
 // max |x| over n floats, atomically maxed (as float bits) into *amax (F16 tower scaling):
 // float4 grid-stride loads, one atomic per workgroup.
@@ -1395,6 +1401,15 @@ static void set_tower_attrs()
     SDE_WINO_ATTR(false, false, true);
     SDE_WINO_ATTR(false, false, false);
 #undef SDE_WINO_ATTR
+#define SDE_SKEW_ATTR(F, I, O) (void)hipFuncSetAttribute((const void *)conv64_skew_kernel<F, I, O>, \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, SK_SMEM)
+    SDE_SKEW_ATTR(true, false, true);
+    SDE_SKEW_ATTR(true, false, false);
+    SDE_SKEW_ATTR(false, true, true);
+    SDE_SKEW_ATTR(false, true, false);
+    SDE_SKEW_ATTR(false, false, true);
+    SDE_SKEW_ATTR(false, false, false);
+#undef SDE_SKEW_ATTR
     });
 }
 
@@ -1464,6 +1479,16 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         bt.pix_stride = (int64_t)hout * wout;
         bt.amax_stride = amax_stride;
         const int grid = std::min(bt.ntiles, cu_count());
+        if (TOWER_SKEW && f16 && !last) {
+            // the two M-tiles of a tile on two waves per SIMD, one c-block apart (tower_skew.h)
+#define SDE_SKEW(F, I, O) conv64_skew_kernel<F, I, O><<<grid, 768, SK_SMEM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, \
+                                                                               out, hout, wout, bt, in_amax, out_amax)
+            if (layer == 2) { if (out_cb) SDE_SKEW(true, false, true); else SDE_SKEW(true, false, false); }
+            else if (in_cb) { if (out_cb) SDE_SKEW(false, true, true); else SDE_SKEW(false, true, false); }
+            else { if (out_cb) SDE_SKEW(false, false, true); else SDE_SKEW(false, false, false); }
+#undef SDE_SKEW
+            return;
+        }
 #define SDE_X6P(F, L, I, O, H) conv64_x6p_kernel<F, L, I, O, H><<<grid, 512, XP_SMEM, st>>>( \
         in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
         (L) ? onrm : nullptr, bt, in_amax, out_amax)

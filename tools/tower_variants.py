@@ -68,5 +68,12 @@ for rnd in range(3):
                                              ws.data_ptr(), nws, 8, None, None, None, s)
             assert rc == 0, rc
         res.setdefault((name, "tower pair f16x3"), []).append(timed(runb, 10))
+        if rnd == 0:   # features bit-identical to the first library's
+            runb()
+            torch.cuda.synchronize()
+            if name == libs[0][0]:
+                ref_feat = feat.clone()
+            print(f"{name:20s} tower pair features identical to {libs[0][0]}: {torch.equal(feat, ref_feat)}",
+                  flush=True)
 for (name, what), v in res.items():
     print(f"{name:20s} {what:18s} {statistics.median(v):8.1f} us   ({' '.join(f'{t:.0f}' for t in v)})", flush=True)
