@@ -306,3 +306,30 @@ def test_cvlr_volumes_repeatable_vs_oracle(gpu, oracle):
     ol, orr = oracle.cost_volume_hwd(host(fl), host(fr), D, invalid=1.0, right=True)
     assert host(outs[0][0]).tobytes() == ol.view(np.int32).tobytes()
     assert host(outs[0][1]).tobytes() == orr.view(np.int32).tobytes()
+
+
+@pytest.mark.parametrize("D,d0", [(192, 0), (96, 0), (64, 17), (40, 0), (160, 33), (33, 0), (1, 0), (2, 31)])
+def test_certified_cv_wta_pipelined_sweep_repeatable(gpu, D, d0):
+    """The software-pipelined tile sweep of the certified CV+WTA (cv_row.hip) over band widths that
+    leave 1, 2, 3 and more right tiles per pixel group (the sweep's tails), W not a multiple of the
+    superstrip, repeated textures (exact ties -> fix-ups): 6 launches give the same bits and fix-up
+    count, equal to the exact kernel's disparities and min costs."""
+    from scenedepthestimation_amd import ops
+    from scenedepthestimation_amd.synthetic import features
+    H, W = 24, 1000
+    fl, fr = features(H, W, seed=11), features(H, W, seed=12)
+    fr[:, 300:340] = fr[:, 260:300]           # repeated texture: exact cost ties
+    fl[:, 500:520] = 0.0                      # zero features: all-zero scores
+    fl, fr = dev(fl), dev(fr)
+    ws = torch.empty(ops.cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device="cuda")
+    outs = []
+    for _ in range(6):
+        _, mn, am = ops.cv_wta(fl, fr, d0, d0 + D, want=("min", "argmin"), mode="certified", workspace=ws)
+        outs.append((mn.view(torch.int32).clone(), am.clone(), ops.cv_wta_fixups(ws)))
+    for mn, am, nf in outs[1:]:
+        assert torch.equal(mn, outs[0][0]) and torch.equal(am, outs[0][1]) and nf == outs[0][2]
+    _, emn, eam = ops.cv_wta(fl, fr, d0, d0 + D, want=("min", "argmin"), mode="exact")
+    assert torch.equal(outs[0][1], eam)
+    assert torch.equal(outs[0][0], emn.view(torch.int32))
+    if D > 1:
+        assert outs[0][2] > 0                 # the ties and zero rows went to the exact fix-up
