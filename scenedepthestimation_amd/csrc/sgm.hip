@@ -38,6 +38,12 @@
 #ifndef SGM_FENCE
 #define SGM_FENCE 0   // profiling builds: a scheduling fence between a step's use of its slot and the refill
 #endif
+// Fused WTA bookkeeping: 1 parks each step's S values in LDS and scans a pixel's D values in d
+// order spread over the next block's steps (no per-step lane-local argmin, no index tie-breaks
+// until the G-lane DPP merge); 0 the round-3 lane-partial form (A/B builds).
+#ifndef SGM_WTA_PARK
+#define SGM_WTA_PARK 1
+#endif
 
 namespace sde {
 
@@ -90,6 +96,18 @@ __device__ __forceinline__ double dpp_f64(double v)
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
+// DPP move of a double for reductions whose disabled lanes are never read: no `old` operand, so
+// the compiler emits the two v_mov_b32_dpp into fresh registers (dpp_f64's old = v costs two
+// v_mov copies per stage).  Lanes outside ROW_MASK hold unspecified values.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dpp_f64_nold(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, ROW_MASK, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
 // t < a ? t : a.  VMIN: one v_min_f64 instead of a compare and two selects.  The two differ
 // only when a is NaN or both are zeros of opposite signs.  In the fast recurrence no operand
 // is NaN (non-finite costs and penalties take the faithful path), and a zero's sign never
@@ -107,16 +125,19 @@ __device__ __forceinline__ double dmin(double a, double t)
     return t < a ? t : a;
 }
 
-// min over the 64 lanes, returned wave-uniform
+// min over the 64 lanes, returned wave-uniform.  Only lane 63 is read: stages 1-4 move within
+// rows (every lane valid); stage 5 updates rows 1 and 3 from lanes 15 and 47, stage 6 row 3 from
+// lane 31 (row 1, valid after stage 5) -- the rows a stage leaves out hold unspecified values
+// and never feed lane 63, so the moves need no `old` operand.
 template <bool VMIN = false>
 __device__ __forceinline__ double wave_min_f64(double v)
 {
-    v = dmin<VMIN>(v, dpp_f64<0xB1>(v));          // quad_perm [1,0,3,2]
-    v = dmin<VMIN>(v, dpp_f64<0x4E>(v));          // quad_perm [2,3,0,1]
-    v = dmin<VMIN>(v, dpp_f64<0x124>(v));         // row_ror:4
-    v = dmin<VMIN>(v, dpp_f64<0x128>(v));         // row_ror:8   -> every lane holds its row's min
-    v = dmin<VMIN>(v, dpp_f64<0x142, 0xA>(v));    // row_bcast:15 -> rows 1, 3
-    v = dmin<VMIN>(v, dpp_f64<0x143, 0xC>(v));    // row_bcast:31 -> row 3 holds all four
+    v = dmin<VMIN>(v, dpp_f64_nold<0xB1>(v));          // quad_perm [1,0,3,2]
+    v = dmin<VMIN>(v, dpp_f64_nold<0x4E>(v));          // quad_perm [2,3,0,1]
+    v = dmin<VMIN>(v, dpp_f64_nold<0x124>(v));         // row_ror:4
+    v = dmin<VMIN>(v, dpp_f64_nold<0x128>(v));         // row_ror:8   -> every lane holds its row's min
+    v = dmin<VMIN>(v, dpp_f64_nold<0x142, 0xA>(v));    // row_bcast:15 -> rows 1, 3
+    v = dmin<VMIN>(v, dpp_f64_nold<0x143, 0xC>(v));    // row_bcast:31 -> row 3 holds all four
     const long long b = __builtin_bit_cast(long long, v);
     const int lo = __builtin_amdgcn_readlane((int)b, 63);
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
@@ -484,9 +505,17 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     // stays one uniform step: a separate merge block after every PF steps made the compiler rotate
     // the prefetch ring's registers at the loop back-edge and drain it (vmcnt(0) every PF steps).
     // Partials and pixel indices are double-buffered by block parity.
-    constexpr int G = 64 / PF, WS = 64 + G;
-    __shared__ float wbv[WTA ? 2 * PF * WS : 1];
-    __shared__ int wba[WTA ? 2 * PF * WS : 1];
+    //
+    // SGM_WTA_PARK (the default): each step parks its 64 DPL S values (+inf past D) in a row of RS =
+    // 64 DPL + 1 words, and lane (st, q) scans pixel st's disparities DPL (PF q + j) + i, i < DPL, at
+    // step j of the next block -- the values lane PF q + j parked -- in increasing d with a strict `<`
+    // (the reference's sequential scan over its chunk), so only the G-lane DPP merge needs the index
+    // tie-break.  The per-step writes (stride DPL) and reads (row stride RS = 1 mod 64 words, lane
+    // chunks 8 DPL apart for PF = 8) are bank-conflict-free at DPL = 3.
+    constexpr int G = 64 / PF, WS = 64 + G, RS = 64 * DPL + 1;
+    constexpr bool PARK = SGM_WTA_PARK != 0;
+    __shared__ float wbv[WTA ? 2 * PF * (PARK ? RS : WS) : 1];
+    __shared__ int wba[WTA && !PARK ? 2 * PF * WS : 1];
     __shared__ int wpx[WTA ? 2 * PF : 1];
     __shared__ FaithLds<DPL> flds;
 
@@ -581,7 +610,33 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     o[i] = (float)((double)o[i] + (du_first ? c : c + 0.0));
                 }
             }
-            if (WTA) {
+            if (WTA && PARK) {
+                // this step's S values parked; one piece of the previous block's scan (below), off
+                // the recurrence's serial chain
+                float *row = wbv + (buf * PF + j) * RS + dbase;
+#pragma unroll
+                for (int i = 0; i < DPL; i++) row[i] = (DC || dbase + i < D) ? o[i] : __builtin_inff();
+                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+                if (k0 > 0) {
+                    const int d0 = DPL * (PF * wq + j);
+                    const float *src = wbv + ((buf ^ 1) * PF + wst) * RS + d0;
+#pragma unroll
+                    for (int i = 0; i < DPL; i++) {
+                        const float v2 = src[i];
+                        if (j == 0 && i == 0) {
+                            // the chunk's first value; a NaN S(0) makes the pixel's answer 0
+                            const bool w = v2 < __builtin_inff();
+                            mv_b = w ? v2 : __builtin_inff();
+                            mv_a = w ? d0 : 0x7fffffff;
+                            if (wq == 0 && v2 != v2) { mv_b = -__builtin_inff(); mv_a = 0; }
+                        } else if (v2 < mv_b) {
+                            mv_b = v2;
+                            mv_a = d0 + i;
+                        }
+                    }
+                    if (j == PF - 1) wta_block_store<G>(mv_b, mv_a, wpx[(buf ^ 1) * PF + wst], wq, sd.disp);
+                }
+            } else if (WTA) {
                 // lane-local first-min over this lane's disparities, parked in LDS; the 64-way
                 // merge runs once per PF steps (below), off the recurrence's serial chain
                 float bv = __builtin_inff();
@@ -637,7 +692,18 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             ahead.advance(g);
         }
     }
-    if (WTA && g.n > 0) {
+    if (WTA && PARK && g.n > 0) {
+        // the last block's scan (its values are in buffer buf_last)
+        const int buf = ((g.n - 1) / PF) & 1;
+        const float *src = wbv + (buf * PF + wst) * RS + DPL * PF * wq;
+        float b = __builtin_inff();
+        int ba = 0x7fffffff;
+#pragma unroll
+        for (int t = 0; t < DPL * PF; t++)
+            if (src[t] < b) { b = src[t]; ba = DPL * PF * wq + t; }
+        if (wq == 0 && src[0] != src[0]) { b = -__builtin_inff(); ba = 0; }
+        wta_block_store<G>(b, ba, wpx[buf * PF + wst], wq, sd.disp);
+    } else if (WTA && g.n > 0) {
         // the last block's merge (its partials are in buffer buf_last)
         const int buf = ((g.n - 1) / PF) & 1;
         float b = wbv[(buf * PF + wst) * WS + wq];
