@@ -381,28 +381,66 @@ template <int DPL>
 struct Slot {
     float c[DPL];
     float s[DPL];
-    float p1, p2;   // p1 as loaded: the step applies `pin` (a select at issue would wait for the load)
+    float p1, p2;   // p1 as loaded: the step applies `pin` (a select at issue would wait for the load);
+                    // SGM_WALK: this pixel's P1 channel, the NEXT step's P1
     size_t off;     // voxel offset of (r, c, d = 0)
     bool restart;
-    bool pin;       // the previous pixel is inside the image (else P1 = 0)
+    bool pin;       // the previous pixel is inside the image (else P1 = 0); unused under SGM_WALK
 };
 
 // Incremental walk along a scanline (wave-uniform scalars; no divisions).  Same
 // pixel sequence as path_pixel: diagonal lines wrap around the image with a
 // path restart.  Steps past the end of the line are clamped into the image (the
 // kernel re-reads valid memory there and stores nothing).
+// SGM_WALK (the default): the pixel index itself advances (one 64-bit scalar add per step, and a
+// +-W on a diagonal wrap) and stops at the line's last pixel, instead of clamping (r, c) and
+// recomputing r W + c and the previous pixel's index with 64-bit multiplies on every step.  A
+// step's predecessor on the path is the previous step's pixel unless the step restarts the path
+// (line start, diagonal wrap), which is exactly when the reference's P1 pixel is outside the
+// image -- so P1 is carried from the previous step and one 8-byte load per step fetches (P1, P2)
+// of the pixel (channels ch, ch + 1; ch even).
+#ifndef SGM_WALK
+#define SGM_WALK 1
+#endif
+#ifndef SGM_EDGESEL
+#define SGM_EDGESEL 1  // D = 64 DPL kernels: the edge lanes' missing neighbours by selects, not branches
+#endif
 struct Walker {
     int r, c;
     bool restart;
+    int left;           // SGM_WALK: moves left before the line's last pixel
+    long long dpx;      // SGM_WALK: pixel-index step dr W + dc
+    size_t px;          // SGM_WALK: the pixel index r W + c
     __device__ __forceinline__ void init(const PathGeom &g, int line)
     {
         if (g.dc == 0) { c = line; r = g.dr > 0 ? 0 : g.H - 1; }
         else if (g.dr == 0) { r = line; c = g.dc > 0 ? 0 : g.W - 1; }
         else { r = g.dr > 0 ? 0 : g.H - 1; c = line; }
         restart = true;
+        if (SGM_WALK) {
+            const int nlen = (g.dc != 0 && g.dr == 0) ? g.W : g.H;
+            left = min(g.n, nlen) - 1;
+            dpx = (long long)g.dr * g.W + g.dc;
+            px = (size_t)r * g.W + c;
+        }
     }
     __device__ __forceinline__ void advance(const PathGeom &g)
     {
+        if (SGM_WALK) {
+            // selects, not branches (scalar s_cselect; the step is one basic block)
+            const bool mv = left > 0;
+            left -= mv ? 1 : 0;
+            c += mv ? g.dc : 0;
+            px += mv ? dpx : 0;
+            restart = false;
+            if (g.dr != 0 && g.dc != 0) {
+                const bool wr = g.dc > 0 ? c >= g.W : c < 0;
+                c = wr ? (g.dc > 0 ? 0 : g.W - 1) : c;
+                px = wr ? (g.dc > 0 ? px - g.W : px + g.W) : px;
+                restart = wr;
+            }
+            return;
+        }
         r += g.dr;
         c += g.dc;
         restart = false;
@@ -419,26 +457,37 @@ template <int DPL, bool VEC, bool FIRST>
 __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const SgmSide &sd, int D, int dbase,
                                       Slot<DPL> &sl)
 {
-    const int r = min(max(w.r, 0), g.H - 1), c = min(max(w.c, 0), g.W - 1);
-    const size_t px = (SGM_DIAG & 1) ? (size_t)(c & 63) : (size_t)r * g.W + c;
-    int pr = r - g.dr, pc = c - g.dc;
-    const bool pin = pr >= 0 && pr < g.H && pc >= 0 && pc < g.W;
-    pr = pin ? pr : r;
-    pc = pin ? pc : c;
-    sl.p1 = sd.pen[((size_t)pr * g.W + pc) * 16 + g.ch];
-    sl.pin = pin;
-    sl.p2 = sd.pen[px * 16 + g.ch + 1];
+    size_t px;
+    if (SGM_WALK) {
+        px = (SGM_DIAG & 1) ? (size_t)(w.c & 63) : w.px;
+        const float2 pp = *reinterpret_cast<const float2 *>(sd.pen + px * 16 + g.ch);
+        sl.p1 = pp.x;
+        sl.p2 = pp.y;
+    } else {
+        const int r = min(max(w.r, 0), g.H - 1), c = min(max(w.c, 0), g.W - 1);
+        px = (SGM_DIAG & 1) ? (size_t)(c & 63) : (size_t)r * g.W + c;
+        int pr = r - g.dr, pc = c - g.dc;
+        const bool pin = pr >= 0 && pr < g.H && pc >= 0 && pc < g.W;
+        pr = pin ? pr : r;
+        pc = pin ? pc : c;
+        sl.p1 = sd.pen[((size_t)pr * g.W + pc) * 16 + g.ch];
+        sl.pin = pin;
+        sl.p2 = sd.pen[px * 16 + g.ch + 1];
+    }
     sl.restart = w.restart;
     const size_t off = px * D;
     sl.off = off;
     if (VEC) {
         const size_t o = off + (dbase < D ? dbase : 0);
         if (SGM_NT & 1) {
+            // wave-uniform row pointers + a 32-bit lane offset: the loads take the SGPR-base form
+            const float *cvp = sd.cv + off, *sp = sd.S + off;
+            const unsigned lo = (unsigned)(dbase < D ? dbase : 0);
 #pragma unroll
-            for (int i = 0; i < DPL; i++) sl.c[i] = __builtin_nontemporal_load(sd.cv + o + i);
+            for (int i = 0; i < DPL; i++) sl.c[i] = __builtin_nontemporal_load(cvp + lo + i);
             if (!FIRST)
 #pragma unroll
-                for (int i = 0; i < DPL; i++) sl.s[i] = __builtin_nontemporal_load(sd.S + o + i);
+                for (int i = 0; i < DPL; i++) sl.s[i] = __builtin_nontemporal_load(sp + lo + i);
         } else {
         const FVec<DPL> cv = *reinterpret_cast<const FVec<DPL> *>(sd.cv + o);
 #pragma unroll
@@ -553,6 +602,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
 
     double L[DPL];
     double m = 1.0, mP2 = 1.0;
+    float p1c = 0.0f;              // SGM_WALK: the previous step's pixel's P1 channel
     int kf = -1;                   // first step with a non-finite cost: the line continues faithfully
     bool redo = false;             // DU fold (FIRST): recompute the column in the faithful arithmetic
 #pragma unroll
@@ -569,7 +619,8 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         for (int j = 0; j < PF; j++) {
             const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
             const Slot<DPL> &sl = ring[j];
-            const float p1f = sl.pin ? sl.p1 : 0.0f, p2f = sl.p2;
+            const float p1f = SGM_WALK ? (sl.restart ? 0.0f : p1c) : (sl.pin ? sl.p1 : 0.0f), p2f = sl.p2;
+            if (SGM_WALK) p1c = sl.p1;      // read before the slot's refill at the end of this step
             if (DU) {
                 if (FIRST && !redo) redo = any_nonfinite<DPL>(sl.c, p1f, p2f);
             } else if (kf < 0 && k < g.n && any_nonfinite<DPL>(sl.c, p1f, p2f)) {
@@ -592,8 +643,16 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     double b = L[i];
                     const double left = i > 0 ? L[i - 1] : lo;
                     const double right = i < DPL - 1 ? L[i + 1] : hi;
-                    if (d > 0) b = dmin<VMIN>(b, left + p1);
-                    if (d < D - 1) b = dmin<VMIN>(b, right + p1);
+                    if (DC && SGM_EDGESEL) {
+                        // D = 64 DPL: only lane 0's first and lane 63's last disparity lack a
+                        // neighbour -- a select of +inf (min(b, inf) = b) instead of an exec-masked
+                        // branch per step
+                        b = dmin<VMIN>(b, (i > 0 || d > 0) ? left + p1 : INF);
+                        b = dmin<VMIN>(b, (i < DPL - 1 || d < D - 1) ? right + p1 : INF);
+                    } else {
+                        if (d > 0) b = dmin<VMIN>(b, left + p1);
+                        if (d < D - 1) b = dmin<VMIN>(b, right + p1);
+                    }
                     b = dmin<VMIN>(b, mP2);
                     Ln[i] = (double)sl.c[i] + (b - m);
                 }
@@ -666,7 +725,8 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                         for (int i = 0; i < DPL; i++) ov.v[i] = o[i];
                         if (SGM_NT & 2) {
 #pragma unroll
-                            for (int i = 0; i < DPL; i++) __builtin_nontemporal_store(o[i], sd.S + sl.off + dbase + i);
+                            for (int i = 0; i < DPL; i++)
+                                __builtin_nontemporal_store(o[i], sd.S + sl.off + (unsigned)dbase + i);
                         } else {
                             *reinterpret_cast<FVec<DPL> *>(sd.S + sl.off + dbase) = ov;
                         }
