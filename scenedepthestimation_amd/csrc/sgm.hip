@@ -384,6 +384,7 @@ struct Slot {
     float p1, p2;   // p1 as loaded: the step applies `pin` (a select at issue would wait for the load);
                     // SGM_WALK: this pixel's P1 channel, the NEXT step's P1
     size_t off;     // voxel offset of (r, c, d = 0)
+    int pix;        // pixel index r W + c (the fused WTA's output index; no 64-bit division by D per step)
     bool restart;
     bool pin;       // the previous pixel is inside the image (else P1 = 0); unused under SGM_WALK
 };
@@ -478,6 +479,7 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
         sl.p2 = sd.pen[px * 16 + g.ch + 1];
     }
     sl.restart = w.restart;
+    sl.pix = (int)px;
     const size_t off = px * D;
     sl.off = off;
     if (VEC) {
@@ -558,13 +560,17 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     // the prefetch ring's registers at the loop back-edge and drain it (vmcnt(0) every PF steps).
     // Partials and pixel indices are double-buffered by block parity.
     //
-    // SGM_WTA_PARK (the default): each step parks its 64 DPL S values (+inf past D) in a row of RS =
-    // 64 DPL + 1 words, and lane (st, q) scans pixel st's disparities DPL (PF q + j) + i, i < DPL, at
-    // step j of the next block -- the values lane PF q + j parked -- in increasing d with a strict `<`
-    // (the reference's sequential scan over its chunk), so only the G-lane DPP merge needs the index
-    // tie-break.  The per-step writes (stride DPL) and reads (row stride RS = 1 mod 64 words, lane
-    // chunks 8 DPL apart for PF = 8) are bank-conflict-free at DPL = 3.
-    constexpr int G = 64 / PF, WS = 64 + G, RS = 64 * DPL + 1;
+    // SGM_WTA_PARK (the default): each step parks its 64 DPL S values (+inf past D), value i of lane
+    // l at word i IS + l of a row of RS words, and lane (st, q) scans pixel st's disparities
+    // DPL (PF q + j) + i, i < DPL, at step j of the next block -- the values lane PF q + j parked --
+    // in increasing d with a strict `<` (the reference's sequential scan over its chunk), so only the
+    // G-lane DPP merge needs the index tie-break.  Banks (PF = 8): RS = 1 mod 64 puts pixel st's row
+    // st banks over, lanes q of a read are 8 banks apart, and IS = 4 mod 64 sends the second word of
+    // the compiler's paired `ds_read2_b32` to the other 4 banks of each 8: writes and reads are
+    // conflict-free (a [lane][i] row with stride DPL had the pair's words collide: 12.6 M conflict
+    // cycles per pair of launches).
+    constexpr int IS = 68, RS = ((DPL * IS + 63) / 64) * 64 + 1;
+    constexpr int G = 64 / PF, WS = 64 + G;
     constexpr bool PARK = SGM_WTA_PARK != 0;
     __shared__ float wbv[WTA ? 2 * PF * (PARK ? RS : WS) : 1];
     __shared__ int wba[WTA && !PARK ? 2 * PF * WS : 1];
@@ -679,16 +685,16 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             if (WTA && PARK) {
                 // this step's S values parked; one piece of the previous block's scan (below), off
                 // the recurrence's serial chain
-                float *row = wbv + (buf * PF + j) * RS + dbase;
+                float *row = wbv + (buf * PF + j) * RS + lane;
 #pragma unroll
-                for (int i = 0; i < DPL; i++) row[i] = (DC || dbase + i < D) ? o[i] : __builtin_inff();
-                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+                for (int i = 0; i < DPL; i++) row[i * IS] = (DC || dbase + i < D) ? o[i] : __builtin_inff();
+                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? sl.pix : -1;
                 if (k0 > 0) {
                     const int d0 = DPL * (PF * wq + j);
-                    const float *src = wbv + ((buf ^ 1) * PF + wst) * RS + d0;
+                    const float *src = wbv + ((buf ^ 1) * PF + wst) * RS + PF * wq + j;
 #pragma unroll
                     for (int i = 0; i < DPL; i++) {
-                        const float v2 = src[i];
+                        const float v2 = src[i * IS];
                         if (j == 0 && i == 0) {
                             // the chunk's first value; a NaN S(0) makes the pixel's answer 0
                             const bool w = v2 < __builtin_inff();
@@ -714,7 +720,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                 const int slot = (buf * PF + j) * WS + (lane % PF) * G + ((lane / PF) ^ (lane % PF & 4));
                 wbv[slot] = bv;
                 wba[slot] = ba;
-                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? (int)(sl.off / D) : -1;
+                if (lane == 0) wpx[buf * PF + j] = (k < g.n && keep) ? sl.pix : -1;
                 // one step of the previous block's merge (nothing to merge in the first block)
                 if (k0 > 0) {
                     const int rs = ((buf ^ 1) * PF + wst) * WS + j * G + (wq ^ (j & 4));
@@ -770,12 +776,14 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     if (WTA && PARK && g.n > 0) {
         // the last block's scan (its values are in buffer buf_last)
         const int buf = ((g.n - 1) / PF) & 1;
-        const float *src = wbv + (buf * PF + wst) * RS + DPL * PF * wq;
+        const float *src = wbv + (buf * PF + wst) * RS + PF * wq;
         float b = __builtin_inff();
         int ba = 0x7fffffff;
 #pragma unroll
-        for (int t = 0; t < DPL * PF; t++)
-            if (src[t] < b) { b = src[t]; ba = DPL * PF * wq + t; }
+        for (int t = 0; t < DPL * PF; t++) {
+            const float v = src[(t % DPL) * IS + t / DPL];      // d = DPL (PF wq + t / DPL) + t % DPL
+            if (v < b) { b = v; ba = DPL * PF * wq + t; }
+        }
         if (wq == 0 && src[0] != src[0]) { b = -__builtin_inff(); ba = 0; }
         wta_block_store<G>(b, ba, wpx[buf * PF + wst], wq, sd.disp);
     } else if (WTA && g.n > 0) {
