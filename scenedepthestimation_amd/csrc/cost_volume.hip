@@ -668,6 +668,9 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
 //     the next own pixels' DMA, dots, barrier, the next rows' DMA.
 // Voxels with x >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
+#ifndef C3_EARLY
+#define C3_EARLY 1    // the strip start waits for the own pixels only; the rows before the second barrier
+#endif
 #ifndef C3_SKIP
 #define C3_SKIP 0     // diagnostic builds only: 2 stores, 4 in-loop DMA, 8 dots
 #endif
@@ -786,8 +789,14 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
         const bool compute = q0 + 16 * wave < W;            // wave-uniform
         const int u = q0 + 16 * wave + 2 * p;
         // this strip's rows and own pixels have landed (every wave's DMA, hence the barrier); the
-        // previous strip's tile is complete
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // previous strip's tile is complete.  C3_EARLY: only the own pixels are waited for here --
+        // per wave the ops after them are the previous strip's 32 emission stores (none before
+        // strip 2) and this strip's 4-5 ring DMA instructions, and vmcnt retires in order -- so the
+        // row block's DMA latency overlaps the own copy and the tile reads; the rows are waited for
+        // before the second barrier.
+        if (!C3_EARLY || k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (k == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
         cd_barrier();
         f32x2 own_a[32], own_b[32];
         if (compute) {
@@ -801,6 +810,7 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
             }
         }
         if (k > 0) emit_load();
+        if (C3_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this strip's rows
         cd_barrier();                                       // the own buffers and the tile are free
         if (more && !(C3_SKIP & 4)) own_unit(q0 + C3_NX, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
         {
