@@ -355,8 +355,8 @@ def cpu_model():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)     # ~0.1 s timed at the north star: 10 steps (20 ms) swung 2.05-2.25 ms/pair box to box
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
     ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard", "dshard_rep", "rowband"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
