@@ -668,6 +668,9 @@ __global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restric
 //     the next own pixels' DMA, dots, barrier, the next rows' DMA.
 // Voxels with x >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
+#ifndef C3_AUX
+X
+#endif
 #ifndef C3_EARLY
 #define C3_EARLY 1    // the strip start waits for the own pixels only; the rows before the second barrier
 #endif
@@ -768,13 +771,13 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
             if (n < 16) {
                 const int x = qp + wave + 4 * n;
                 const uint32_t so = x < W ? (uint32_t)(((qp + wave) * D + dc) * 4 + n * rowstep) : C3_SKIPOFF;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d, so, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d, so, C3_AUX);
             } else {
                 const int xr = qp - dc - 63 + 4 * (n - 16) + wave;
                 const uint32_t so = (uint32_t)xr < (uint32_t)W
                                         ? (uint32_t)(((qp - dc - 63 + wave) * D + dc) * 4 + (n - 16) * rowstep)
                                         : C3_SKIPOFF;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d, so, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d, so, C3_AUX);
             }
         }
     };
