@@ -70,6 +70,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cb_rsrc(const void *base, uint
 // are independent, and one launch of both fills the machine in whole rounds of line-waves (a
 // 1024^2 x 192 pass has 3072 line-waves per volume against 2048-2560 resident: alone, its second
 // round runs half empty).
+#ifndef CBCA_PF
+#define CBCA_PF 16    // positions prefetched ahead (A/B builds: 8)
+#endif
 struct CbcaVolumes {
     const float *src[2];
     float *dst[2];
@@ -86,7 +89,7 @@ __device__ __forceinline__ void cbca_scan(const float *__restrict__ src, float *
 {
     constexpr int RS = 2 * R + 2;      // prefix ring: positions [f - 2R - 1, f]; also the unroll
     constexpr int U = R + 1;           // support ring (trailing output reads the slot of f - R)
-    constexpr int PF = 16;             // prefetch distance (vmcnt saturates at 63 outstanding ops)
+    constexpr int PF = CBCA_PF;        // prefetch distance (vmcnt saturates at 63 outstanding ops)
     static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && RS % PF == 0, "ring sizes");
     const int lane = threadIdx.x;
     // Lanes past D work on d = D-1: they compute lane D-1's value and store it to the
