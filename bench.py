@@ -205,8 +205,7 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
                 feats.append(oracle.tower_forward(oracle.pad_image(z, 2 * NLAYERS + 1), hw, hb))
             cl, cr = oracle.cost_volume_hwd(feats[0], feats[1], D, invalid=1.0, right=True)
             al, ar = oracle.cbca_arms(zs[0], CBCA_L1, CBCA_TAU), oracle.cbca_arms(zs[1], CBCA_L1, CBCA_TAU)
-            cl = oracle.cbca(cl, al, ar, "left", CBCA_ITERS)
-            cr = oracle.cbca(cr, ar, al, "right", CBCA_ITERS)
+            cl, cr = oracle.cbca_lr(cl, cr, al, ar, CBCA_ITERS, L1=CBCA_L1)
             dl = oracle.wta_sgm(oracle.sgm_8path(cl, oracle.sgm_penalties(left[:hc, :wc])))
             dr = oracle.wta_sgm(oracle.sgm_8path(cr, oracle.sgm_penalties(right[:hc, :wc])))
             a, _ = oracle.lr_check(dl, dr)
@@ -299,23 +298,30 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     out[prefix + "gpu_path_ms"] = path_ms
     out[prefix + "ms_per_pair_tower_plus_gpu_path"] = tower_ms + path_ms
     kern = {}
-    # cvlr_dma_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes
-    ms = _events_ms(lambda: ops.cost_volume(m.feat[0], m.feat[1], D, layout="HWD", right=True, invalid=1.0,
-                                            out_left=b["cv"][0], out_right=b["cv"][1]))
+    # cvlr3_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes -- the left one only
+    # when the aggregation follows (sde_cbca_lr writes the right one as the aggregated left one's shear)
+    both = m.cbca_iters <= 0
+    ms = _events_ms(lambda: ops.cost_volume(m.feat[0], m.feat[1], D, layout="HWD", right=both, invalid=1.0,
+                                            out_left=b["cv"][0], out_right=b["cv"][1] if both else None))
     cvlr_ms = ms
-    kern["cvlr3_kernel (L/R volumes)"] = (ms, 4.0 * H * W * (2 * NF + 2 * D))
+    kern["cvlr3_kernel (" + ("L/R volumes)" if both else "L volume)")] = \
+        (ms, 4.0 * H * W * (2 * NF + (2 if both else 1) * D))
     if m.cbca_iters > 0:
-        # one CBCA iteration of both sides: H and V pass read + write 4 B/voxel each
-        ms = _events_ms(lambda: ops.cbca_pair(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], m.cbca_L1, 1,
-                                              tmp_l=b["S"][0], tmp_r=b["S"][1]))
-        kern["cbca_scan_kernel (1 iteration, both sides)"] = (ms, 2 * 16.0 * vox)
+        # sde_cbca_lr (definition v2): the left volume's iterations, each a horizontal and a vertical
+        # pass reading + writing 4 B per valid voxel, then the shear into the right volume (4 + 4 B per
+        # valid voxel); valid = right-image pixel inside the image, sum_d H * max(W - d, 0) voxels
+        valid = float(H) * sum(max(W - d, 0) for d in range(D))
+        ms = _events_ms(lambda: ops.cbca_lr(b["cv"][0], b["cv"][1], b["arms"][0], b["arms"][1], m.cbca_L1,
+                                            m.cbca_iters, tmp=b["S"][0], workspace=b["cbca_ws"]))
+        kern[f"cbca_h/v_kernel + cbca_rotate_kernel ({m.cbca_iters} iterations, one volume + shear)"] = \
+            (ms, (16.0 * m.cbca_iters + 8.0) * valid)
     ms = _events_ms(lambda: ops.sgm_8path_wta_pair(b["cv"][0], b["pen"][0], b["S"][0], b["disp"][0], b["cv"][1],
                                                    b["pen"][1], b["S"][1], b["disp"][1], zero_du_penalties=True))
     # per side: UD+DU 8 B/voxel, five passes 12 B, DU-RL + WTA 8 B, + 4 B/pixel of disparity
     kern["sgm_scan_kernel (8 paths + WTA, both sides, 7 launches)"] = (ms, 2 * (76.0 * vox + 4.0 * H * W))
     per = {}
     tb = tt = 0.0
-    tkeys = {"cvlr": "cvlr", "cbca": "cbca_pair_iteration", "sgm_": "sgm_pair"}
+    tkeys = {"cvlr": "cvlr", "cbca": "cbca_lr", "sgm_": "sgm_pair"}
     for k, (ms, byt) in kern.items():
         gbs = byt / (ms * 1e-3) / 1e9
         per[k] = {"ms": ms, "GB": byt / 1e9, "GB_s": gbs, "hbm_frac": gbs / PEAK_HBM_GBS}
@@ -325,9 +331,8 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
         if tr is not None:
             per[k]["traffic_GB"] = tr / 1e9
             per[k]["traffic_source"] = src
-        n = m.cbca_iters if k.startswith("cbca") else 1
-        tb += byt * n
-        tt += ms * n
+        tb += byt
+        tt += ms
     # the L/R volume kernel's other bound: every valid voxel is NumPy's exact fp32 dot product, 64
     # separately rounded products + 64 adds (pairwise tree, 0.0 + s), on the packed-fp32 VALU
     k0 = next(iter(per))
@@ -337,7 +342,7 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     out[prefix + "cv_aggregation_kernels"] = per
     out[prefix + "cv_aggregation_aggregate"] = {
         "ms": tt, "GB": tb / 1e9, "GB_s": tb / (tt * 1e-3) / 1e9, "hbm_frac": tb / (tt * 1e-3) / 1e9 / PEAK_HBM_GBS,
-        "what": f"cvlr + {m.cbca_iters} x CBCA pair iteration + SGM pair on sec. 8(d) algorithmic bytes"}
+        "what": f"cvlr + CBCA ({m.cbca_iters} iterations, sde_cbca_lr) + SGM pair on sec. 8(d) algorithmic bytes"}
     return out
 
 
@@ -460,8 +465,8 @@ def main():
             if k.startswith("sgm"):
                 sgm_ms = v["ms"]
             if k.startswith("cbca"):
-                stages["cbca_pair_iter_ms"] = v["ms"]
-                stages["cbca_pair_iter_hbm_GBs"] = v["GB_s"]
+                stages["cbca_lr_ms"] = v["ms"]
+                stages["cbca_lr_hbm_GBs"] = v["GB_s"]
         stages["sgm_pair_ms"] = sgm_ms
         ach = sgm_bytes / (sgm_ms * 1e-3) / 1e9
         roof = {"kernel": "sgm_scan_kernel (8-path SGM + WTA, both sides, 7 launches: DU folded into UD, WTA "

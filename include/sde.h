@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SDE_ABI_VERSION 2
+#define SDE_ABI_VERSION 3
 
 typedef enum {
     SDE_OK = 0,
@@ -314,26 +314,59 @@ int sde_sgm_direction(const float *cv, const float *pen, int H, int W, int D, in
 int sde_cbca_arms(const float *img, int64_t pitch, int H, int W, int L1, float tau, uint32_t *arms, void *stream);
 
 /*
- * iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv) on an
- * [H][W][D] volume, in place in cv (tmp: same size, scratch).  side
- * SDE_SIDE_LEFT: left-referenced volume, the other pixel is x - d (arms_ref =
- * left image arms, arms_other = right); SDE_SIDE_RIGHT: x + d.  L1 as given to
- * sde_cbca_arms (arms must not exceed L1 - 1).
+ * Definition v2 (round 4; the CPU restatement under oracle/ states it in full): volumes are
+ * aggregated in LEFT coordinates (a right-referenced volume through
+ * R(y,x',d) = L(y,x'+d,d)); voxels whose right-image pixel is outside the
+ * image pass through unchanged; support arms = min(left-image arm, right-image
+ * arm); fp64 prefix chains restart per segment of SDE_CBCA_SEG positions at
+ * kS - (L1 - 1); the mean multiplies by the correctly rounded fp64 1/count.
+ * Consequence: the aggregation of R = shear(L) is shear(aggregation of L).
  */
-int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W, int D,
-             int side, int L1, int iters, void *stream);
+#define SDE_CBCA_SEG 256
+
+/* Workspace of the aggregation entry points (column-major copies of both
+ * images' arms): 8 * W * roundup(H, 4) bytes. */
+size_t sde_cbca_workspace_bytes(int H, int W);
 
 /*
- * sde_cbca on both volumes of a pair in one launch per pass (same results as
- * sde_cbca(cv_l, tmp_l, arms_l, arms_r, SDE_SIDE_LEFT) and sde_cbca(cv_r,
- * tmp_r, arms_r, arms_l, SDE_SIDE_RIGHT)); the four buffers must be distinct.
+ * iters x (horizontal pass, vertical pass) on an [H][W][D] volume, in place
+ * in cv (tmp: same size, scratch).  side SDE_SIDE_LEFT: left-referenced volume,
+ * the other pixel is x - d (arms_ref = left image arms, arms_other = right);
+ * SDE_SIDE_RIGHT: x + d (arms_ref = right image, arms_other = left; done as a
+ * rotation into left coordinates, the aggregation, and the rotation back).
+ * L1 as given to sde_cbca_arms (arms must not exceed L1 - 1).
+ */
+int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W, int D,
+             int side, int L1, int iters, void *ws, size_t ws_bytes, void *stream);
+
+/*
+ * sde_cbca on both volumes of a pair (same results as sde_cbca(cv_l, tmp_l,
+ * arms_l, arms_r, SDE_SIDE_LEFT) and sde_cbca(cv_r, tmp_r, arms_r, arms_l,
+ * SDE_SIDE_RIGHT)) for any two volumes; the four buffers must be distinct.
  * Build-defined like sde_cbca: the reference only names the aggregated
  * volumes d_cost_volumel/r_after_aggr (process_functional.py:268,347).
  */
 int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_r, const uint32_t *arms_l,
-                  const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *stream);
-/* sde_cbca / sde_cbca_pair shape limits (32-bit scan offsets, refused with SDE_ERR_ARG):
- * H, W <= 65535, 4*H*W < 2^31 and (3R + 18) * 4*W*D < 2^31 with R = 15 (L1 <= 16) or 31. */
+                  const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *ws, size_t ws_bytes,
+                  void *stream);
+
+/*
+ * The GPU path's pair (d_cost_volumel/r_after_aggr, process_functional.py:268,
+ * 347): cv_l aggregated in place (tmp: scratch), then every valid voxel of cv_r
+ * set to its shear, cv_r(y,x',d) = cv_l(y,x'+d,d) for x'+d < W (the others are
+ * left as they are).  Equals sde_cbca_pair whenever cv_r's valid voxels are
+ * the shear of cv_l's -- as sde_cost_volume(..., SDE_LAYOUT_HWD) writes them --
+ * at half its traffic: one volume aggregated, one shear.
+ */
+int sde_cbca_lr(float *cv_l, float *cv_r, float *tmp, const uint32_t *arms_l, const uint32_t *arms_r, int H, int W,
+                int D, int L1, int iters, void *ws, size_t ws_bytes, void *stream);
+/* sde_cbca* shape limits (32-bit offsets, refused with SDE_ERR_ARG): D <= 512,
+ * (5R + 5) * 4*W*D < 2^31 with R = 13 (L1 <= 14), 15 (L1 <= 16) or 31, and
+ * 4 * roundup(H, 4) * W < 2^31. */
+
+/* The fp64 reciprocals the aggregation multiplies by, out[i] = 1/(i+1) as the
+ * kernels compute it (the tests check them against the IEEE quotient). */
+int sde_cbca_reciprocals(double *out, int n, void *stream);
 
 /* is_error_match_kernel (process_functional.py:977-1000): lrc_l/lrc_r u8 [H][W], caller-zeroed. */
 int sde_lr_check(const float *disp_l, const float *disp_r, int H, int W, uint8_t *lrc_l, uint8_t *lrc_r,

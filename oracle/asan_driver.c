@@ -88,9 +88,11 @@ static void run_cbca(int H, int W, int D, int L1)
     sdeo_cbca_arms(img, W, H, W, L1, 0.05f, a);
     sdeo_cbca_arms(img2, W, H, W, L1, 0.05f, b);
     float *cv = fbuf((size_t)H * W * D), *tmp = fbuf((size_t)H * W * D);
-    sdeo_cbca(cv, tmp, a, b, H, W, D, 1, 2);
-    sdeo_cbca(cv, tmp, b, a, H, W, D, 2, 1);
-    free(img); free(img2); free(a); free(b); free(cv); free(tmp);
+    float *cr = fbuf((size_t)H * W * D);
+    sdeo_cbca(cv, tmp, a, b, H, W, D, 1, L1, 2);
+    sdeo_cbca(cv, tmp, b, a, H, W, D, 2, L1, 1);
+    sdeo_cbca_lr(cv, cr, tmp, a, b, H, W, D, L1, 1);
+    free(img); free(img2); free(a); free(b); free(cv); free(tmp); free(cr);
 }
 
 int main(void)
@@ -112,6 +114,8 @@ int main(void)
         run_cbca(9, 13, 6, 32);
         run_cbca(1, 40, 3, 14);
         run_cbca(40, 1, 3, 14);
+        run_cbca(270, 300, 3, 14);     /* two segments each way (CBCA_SEG = 256) */
+        run_cbca(3, 5, 9, 2);          /* D > W */
     }
     printf("asan driver ok\n");
     return 0;

@@ -57,7 +57,9 @@ def lib():
         _u32p = ctypes.POINTER(ctypes.c_uint32)
         L.sdeo_cbca_arms.argtypes = [_f32p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                      _u32p]
-        L.sdeo_cbca.argtypes = [_f32p, _f32p, _u32p, _u32p] + [ctypes.c_int] * 5
+        L.sdeo_cbca.argtypes = [_f32p, _f32p, _u32p, _u32p] + [ctypes.c_int] * 6
+        L.sdeo_cbca_lr.argtypes = [_f32p, _f32p, _f32p, _u32p, _u32p] + [ctypes.c_int] * 5
+        L.sdeo_cbca_seg.restype = ctypes.c_int
         _lib = L
         L.sdeo_set_threads(int(os.environ.get("SDE_ORACLE_THREADS", min(16, os.cpu_count() or 1))))
     return _lib
@@ -269,14 +271,42 @@ def cbca_arms(img, L1=14, tau=0.02):
     return out
 
 
-def cbca(cv_hwd, arms_ref, arms_other, side="left", iters=1):
-    """iters x (horizontal then vertical cross-support mean) of an [H,W,D] volume (new array)."""
+def cbca_seg():
+    """Segment length of the CBCA definition (SDE_CBCA_SEG)."""
+    return int(lib().sdeo_cbca_seg())
+
+
+def _arms(a, L1):
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    M = max(int(L1) - 1, 0)
+    for k in range(4):   # the definition's windows reach at most M = L1 - 1 positions per arm
+        if ((a >> (8 * k)) & 255).max(initial=0) > M:
+            raise ValueError(f"arms exceed L1 - 1 = {M}")
+    return a
+
+
+def cbca(cv_hwd, arms_ref, arms_other, side="left", iters=1, L1=14):
+    """iters x (horizontal then vertical cross-support mean) of an [H,W,D] volume (new array);
+    definition v2 (sde_oracle.c): left coordinates, segmented prefix chains, invalid voxels kept."""
     cv = np.array(cv_hwd, dtype=np.float32, order="C", copy=True)
     H, W, D = cv.shape
     tmp = np.empty_like(cv)
     u32p = ctypes.POINTER(ctypes.c_uint32)
-    a = np.ascontiguousarray(arms_ref, dtype=np.uint32)
-    b = np.ascontiguousarray(arms_other, dtype=np.uint32)
+    a, b = _arms(arms_ref, L1), _arms(arms_other, L1)
     lib().sdeo_cbca(_p(cv), _p(tmp), a.ctypes.data_as(u32p), b.ctypes.data_as(u32p), H, W, D,
-                    1 if side == "left" else 2, int(iters))
+                    1 if side == "left" else 2, int(L1), int(iters))
     return cv
+
+
+def cbca_lr(cv_l, cv_r, arms_l, arms_r, iters=1, L1=14):
+    """sde_cbca_lr: the left volume aggregated, the right one's valid voxels set to its shear
+    (invalid ones kept).  Returns (left, right) as new arrays."""
+    cl = np.array(cv_l, dtype=np.float32, order="C", copy=True)
+    cr = np.array(cv_r, dtype=np.float32, order="C", copy=True)
+    H, W, D = cl.shape
+    tmp = np.empty_like(cl)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    a, b = _arms(arms_l, L1), _arms(arms_r, L1)
+    lib().sdeo_cbca_lr(_p(cl), _p(cr), _p(tmp), a.ctypes.data_as(u32p), b.ctypes.data_as(u32p), H, W, D,
+                       int(L1), int(iters))
+    return cl, cr

@@ -547,26 +547,41 @@ EXPORT void sdeo_tower_forward(const float *img_pad, int Hp, int Wp, int nlayers
 /* Cross-based cost aggregation -- BUILD-DEFINED, PARITY UNPINNED.           */
 /* The reference has none (only the buffer name          */
 /* d_cost_volumel_after_aggr, process_functional.py:268,347, and an unused   */
-/* timer label, match.py:98).  Definition (MC-CNN-style cross support):      */
+/* timer label, match.py:98).  Definition v2 (round 4; MC-CNN-style cross    */
+/* support of both images):                                                  */
 /*  arms: for pixel p and direction left/right/up/down, the largest k in     */
 /*   [0, L1-1] such that every q = p + j*dir, 1 <= j <= k, is inside the     */
 /*   image and fabsf(I(p) - I(q)) < tau (fp32).  Packed l | r<<8 | u<<16 |   */
 /*   d<<24.                                                                  */
-/*  voxel support (p, d): the other image's pixel is o = x - d (left-        */
-/*   referenced volume) or x + d (right-referenced); if o is outside the     */
-/*   image the support is {p}; else every arm is min(ref arm at p, other     */
-/*   arm at o).                                                              */
-/*  one iteration: horizontal pass, then vertical pass, each through an fp64  */
-/*   prefix sum accumulated sequentially from the start of the line:         */
-/*   P(x) = P(x-1) + (double)C(y,x,d), P(-1) = 0,                            */
-/*   T(p,d) = (float)(P(x+hr) - P(x-hl-1));                                  */
-/*   Q(y) = Q(y-1) + (double)T(y,x,d), Q(-1) = 0,                            */
-/*   C'(p,d) = (float)((Q(y+vd) - Q(y-vu-1)) / (double)cnt),                  */
-/*   cnt = sum_{i=-vu..vd} (hl+hr+1)(y+i, x, d) (exact integer): the mean    */
-/*   over the union of the horizontal segments hanging off p's vertical      */
-/*   segment.  (Prefix differences make each voxel O(1) on the GPU; fp64     */
-/*   keeps them accurate to ~1e-16 of the line sum.)                         */
+/*  coordinates: volumes are aggregated in LEFT coordinates q (the left      */
+/*   image's column): a left-referenced volume L(y,q,d) as it is, a right-   */
+/*   referenced one through R(y,x',d) = L(y,x'+d,d).  Voxel (y,q,d) is valid */
+/*   iff its right-image pixel q-d is inside the image (q >= d); an invalid  */
+/*   voxel passes through every pass unchanged.                              */
+/*  support arms of a valid voxel: per direction min(left-image arm at       */
+/*   (y,q), right-image arm at (y,q-d)).  A right-referenced voxel and the   */
+/*   left voxel it shears from have ONE support, so CBCA(R) = shear(CBCA(L)) */
+/*   exactly whenever R = shear(L) (the GPU path's L/R volumes are).         */
+/*  segments: every line is cut into segments of S = CBCA_SEG positions; the */
+/*   prefix chain of segment k starts at b = max(kS - M, first valid         */
+/*   position of the line) with M = L1 - 1 (the longest arm) and             */
+/*   P(b-1) = 0, so both ends of every window of the segment lie on its own  */
+/*   chain (a GPU wave can take any segment with an M-position pre-roll).    */
+/*  horizontal pass, row y, disparity d, valid q in [d, W):                  */
+/*   P(i) = P(i-1) + (double)C(y,i,d),  T(y,q,d) = (float)(P(q+hr) - P(q-hl-1)) */
+/*  vertical pass, column q (valid), disparity d (rows; first valid row 0):  */
+/*   Q(i) = Q(i-1) + (double)T(i,q,d),  N(i) = N(i-1) + hl + hr + 1 at (i,q,d) */
+/*   C'(y,q,d) = (float)((Q(y+vd) - Q(y-vu-1)) * (1.0 / (double)cnt)),       */
+/*   cnt = N(y+vd) - N(y-vu-1) (exact), 1.0/cnt the correctly rounded fp64   */
+/*   reciprocal: the mean over the union of the horizontal segments hanging  */
+/*   off the voxel's vertical segment.                                       */
+/*  one iteration = horizontal pass, then vertical pass.                     */
+/* (v1, rounds 1-3: prefixes from the line start, both volumes aggregated    */
+/* independently, fp64 division.)                                            */
 /* ------------------------------------------------------------------------ */
+#define CBCA_SEG 256 /* = SDE_CBCA_SEG (include/sde.h; test_capi checks they agree) */
+EXPORT int sdeo_cbca_seg(void) { return CBCA_SEG; }
+
 EXPORT void sdeo_cbca_arms(const float *img, long pitch, int H, int W, int L1, float tau, uint32_t *arms)
 {
     static const int dys[4] = {0, 0, -1, 1}, dxs[4] = {-1, 1, 0, 0};
@@ -589,89 +604,150 @@ EXPORT void sdeo_cbca_arms(const float *img, long pitch, int H, int W, int L1, f
         }
 }
 
-static inline void cbca_support(const uint32_t *ref, const uint32_t *oth, int W, int y, int x, int d, int side,
-                                int *a)
+/* support arms of the valid left-coordinate voxel (y, q, d): al / ar = left / right image arms */
+static inline void cbca_support(const uint32_t *al, const uint32_t *ar, int W, int y, int q, int d, int *a)
 {
-    const int o = side == 1 ? x - d : x + d;
-    if (o < 0 || o >= W) { a[0] = a[1] = a[2] = a[3] = 0; return; }
-    const uint32_t p = ref[(size_t)y * W + x], q = oth[(size_t)y * W + o];
+    const uint32_t p = al[(size_t)y * W + q], o = ar[(size_t)y * W + q - d];
     for (int k = 0; k < 4; k++) {
-        const int u = (p >> (8 * k)) & 255, v = (q >> (8 * k)) & 255;
+        const int u = (p >> (8 * k)) & 255, v = (o >> (8 * k)) & 255;
         a[k] = u < v ? u : v;
     }
 }
 
-/* side: 1 = left-referenced volume (other pixel x - d), 2 = right-referenced (x + d).
- * Loops run d innermost (contiguous voxels); every (line, d) prefix is still accumulated
- * sequentially along its line, so the arithmetic is the definition's. */
-EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
-                            int D, int side)
+static inline int imax(int a, int b) { return a > b ? a : b; }
+static inline int imin(int a, int b) { return a < b ? a : b; }
+
+/* Horizontal pass on a left-coordinate volume (src -> dst, [H][W][D]).  Loops run d innermost
+ * (contiguous voxels); every (row, d, segment) chain is still accumulated sequentially in the
+ * definition's order. */
+EXPORT void sdeo_cbca_hpass(const float *src, float *dst, const uint32_t *al, const uint32_t *ar, int H, int W,
+                            int D, int L1)
 {
+    const int M = L1 - 1, S = CBCA_SEG;
 #pragma omp parallel num_threads(g_threads)
     {
-        /* P[(x + 1) * D + d] = prefix of line (y, d) through x; P[d] = 0 */
+        /* P[(i + 1) * D + d] = chain of (y, d, segment) through position i; P[b * D + d] = 0 */
         double *P = (double *)malloc(sizeof(double) * (size_t)(W + 1) * D);
 #pragma omp for schedule(static)
         for (int y = 0; y < H; y++) {
-            for (int d = 0; d < D; d++) P[d] = 0.0;
-            for (int x = 0; x < W; x++)
-                for (int d = 0; d < D; d++)
-                    P[(size_t)(x + 1) * D + d] = P[(size_t)x * D + d] + (double)src[((size_t)y * W + x) * D + d];
-            for (int x = 0; x < W; x++)
-                for (int d = 0; d < D; d++) {
-                    int a[4];
-                    cbca_support(ref, oth, W, y, x, d, side, a);
-                    dst[((size_t)y * W + x) * D + d] =
-                        (float)(P[(size_t)(x + a[1] + 1) * D + d] - P[(size_t)(x - a[0]) * D + d]);
-                }
+            const size_t row = (size_t)y * W * D;
+            for (int q = 0; q < W; q++)
+                for (int d = q + 1; d < D; d++) dst[row + (size_t)q * D + d] = src[row + (size_t)q * D + d];
+            for (int k = 0; k * S < W; k++) {
+                const int t1 = imin((k + 1) * S, W), e = imin(t1 - 1 + M, W - 1), b0 = imax(k * S - M, 0);
+                for (int d = 0; d < D && d <= e; d++) P[(size_t)imax(b0, d) * D + d] = 0.0;
+                for (int i = b0; i <= e; i++)
+                    for (int d = 0; d < D && d <= i; d++)   /* i >= b = max(b0, d) */
+                        P[(size_t)(i + 1) * D + d] = P[(size_t)i * D + d] + (double)src[row + (size_t)i * D + d];
+                for (int q = k * S; q < t1; q++)
+                    for (int d = 0; d < D && d <= q; d++) {
+                        int a[4];
+                        cbca_support(al, ar, W, y, q, d, a);
+                        dst[row + (size_t)q * D + d] =
+                            (float)(P[(size_t)(q + a[1] + 1) * D + d] - P[(size_t)(q - a[0]) * D + d]);
+                    }
+            }
         }
         free(P);
     }
 }
 
-EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *ref, const uint32_t *oth, int H, int W,
-                            int D, int side)
+/* Vertical pass on a left-coordinate volume (src -> dst). */
+EXPORT void sdeo_cbca_vpass(const float *src, float *dst, const uint32_t *al, const uint32_t *ar, int H, int W,
+                            int D, int L1)
 {
+    const int M = L1 - 1, S = CBCA_SEG;
 #pragma omp parallel num_threads(g_threads)
     {
-        /* Q / N[(y + 1) * D + d]: prefix of column (x, d) through row y */
+        /* Q / N[(i + 1) * D + d]: chain of column (q, d, segment) through row i */
         double *Q = (double *)malloc(sizeof(double) * (size_t)(H + 1) * D);
         long *N = (long *)malloc(sizeof(long) * (size_t)(H + 1) * D);
 #pragma omp for schedule(static)
-        for (int x = 0; x < W; x++) {
-            for (int d = 0; d < D; d++) {
-                Q[d] = 0.0;
-                N[d] = 0;
+        for (int q = 0; q < W; q++) {
+            for (int y = 0; y < H; y++)
+                for (int d = q + 1; d < D; d++) {
+                    const size_t v = ((size_t)y * W + q) * D + d;
+                    dst[v] = src[v];
+                }
+            const int dn = imin(D, q + 1);   /* valid disparities of this column: d <= q */
+            for (int k = 0; k * S < H; k++) {
+                const int t1 = imin((k + 1) * S, H), e = imin(t1 - 1 + M, H - 1), b = imax(k * S - M, 0);
+                for (int d = 0; d < dn; d++) {
+                    Q[(size_t)b * D + d] = 0.0;
+                    N[(size_t)b * D + d] = 0;
+                }
+                for (int i = b; i <= e; i++)
+                    for (int d = 0; d < dn; d++) {
+                        int a[4];
+                        cbca_support(al, ar, W, i, q, d, a);
+                        const size_t u = (size_t)(i + 1) * D + d, w = (size_t)i * D + d;
+                        Q[u] = Q[w] + (double)src[((size_t)i * W + q) * D + d];
+                        N[u] = N[w] + a[0] + a[1] + 1;
+                    }
+                for (int y = k * S; y < t1; y++)
+                    for (int d = 0; d < dn; d++) {
+                        int a[4];
+                        cbca_support(al, ar, W, y, q, d, a);
+                        const size_t hi = (size_t)(y + a[3] + 1) * D + d, lo = (size_t)(y - a[2]) * D + d;
+                        const double num = Q[hi] - Q[lo];
+                        const long cnt = N[hi] - N[lo];
+                        dst[((size_t)y * W + q) * D + d] = (float)(num * (1.0 / (double)cnt));
+                    }
             }
-            for (int y = 0; y < H; y++)
-                for (int d = 0; d < D; d++) {
-                    int b[4];
-                    cbca_support(ref, oth, W, y, x, d, side, b);
-                    const size_t i = (size_t)(y + 1) * D + d, j = (size_t)y * D + d;
-                    Q[i] = Q[j] + (double)src[((size_t)y * W + x) * D + d];
-                    N[i] = N[j] + b[0] + b[1] + 1;
-                }
-            for (int y = 0; y < H; y++)
-                for (int d = 0; d < D; d++) {
-                    int a[4];
-                    cbca_support(ref, oth, W, y, x, d, side, a);
-                    const size_t hi = (size_t)(y + a[3] + 1) * D + d, lo = (size_t)(y - a[2]) * D + d;
-                    const double num = Q[hi] - Q[lo];
-                    const long cnt = N[hi] - N[lo];
-                    dst[((size_t)y * W + x) * D + d] = (float)(num / (double)cnt);
-                }
         }
         free(Q);
         free(N);
     }
 }
 
-/* iters x (horizontal pass cv -> tmp, vertical pass tmp -> cv); result in cv. */
-EXPORT void sdeo_cbca(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D, int side,
-                      int iters)
+/* Per-disparity cyclic rotation of every row: out(y, x, d) = in(y, (x + s*d) mod W, d), s = +1 / -1.
+ * s = -1 takes a right-referenced volume to left coordinates (its invalid voxels land on the
+ * left-coordinate invalid ones, q < d), s = +1 takes it back. */
+static void cbca_rotate(const float *in, float *out, int H, int W, int D, int s)
 {
-    for (int it = 0; it < iters; it++) {
-        sdeo_cbca_hpass(cv, tmp, ref, oth, H, W, D, side);
-        sdeo_cbca_vpass(tmp, cv, ref, oth, H, W, D, side);
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D; d++) {
+                const long src = (((long)x + s * (long)(d % W)) % W + W) % W;
+                out[((size_t)y * W + x) * D + d] = in[((size_t)y * W + src) * D + d];
+            }
+}
+
+/* iters x (horizontal pass, vertical pass) of one volume, in place in cv (tmp: scratch of the same
+ * size).  side 1: left-referenced (arms_ref = left image, arms_other = right image); side 2:
+ * right-referenced (arms_ref = right image, arms_other = left image), aggregated in left
+ * coordinates through the rotation above. */
+EXPORT void sdeo_cbca(float *cv, float *tmp, const uint32_t *ref, const uint32_t *oth, int H, int W, int D, int side,
+                      int L1, int iters)
+{
+    if (side == 1) {
+        for (int it = 0; it < iters; it++) {
+            sdeo_cbca_hpass(cv, tmp, ref, oth, H, W, D, L1);
+            sdeo_cbca_vpass(tmp, cv, ref, oth, H, W, D, L1);
+        }
+        return;
     }
+    float *rot = (float *)malloc(sizeof(float) * (size_t)H * W * D);
+    cbca_rotate(cv, rot, H, W, D, -1);
+    for (int it = 0; it < iters; it++) {
+        sdeo_cbca_hpass(rot, tmp, oth, ref, H, W, D, L1);
+        sdeo_cbca_vpass(tmp, rot, oth, ref, H, W, D, L1);
+    }
+    cbca_rotate(rot, cv, H, W, D, +1);
+    free(rot);
+}
+
+/* The GPU path's pair (sde_cbca_lr): the left volume aggregated in place, then every valid voxel of
+ * the right volume set to its shear, cv_r(y, x', d) = cv_l(y, x'+d, d) for x'+d < W (invalid ones
+ * untouched).  Equal to sdeo_cbca(cv_r, side 2) whenever cv_r's valid voxels are cv_l's shear. */
+EXPORT void sdeo_cbca_lr(float *cv_l, float *cv_r, float *tmp, const uint32_t *al, const uint32_t *ar, int H, int W,
+                         int D, int L1, int iters)
+{
+    sdeo_cbca(cv_l, tmp, al, ar, H, W, D, 1, L1, iters);
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int d = 0; d < D && x + d < W; d++)
+                cv_r[((size_t)y * W + x) * D + d] = cv_l[((size_t)y * W + x + d) * D + d];
 }

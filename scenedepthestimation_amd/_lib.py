@@ -21,6 +21,7 @@ c_int, c_int64, c_float, c_double, c_void_p = ctypes.c_int, ctypes.c_int64, ctyp
 c_char_p = ctypes.c_char_p
 
 SDE_OK = 0
+SDE_ABI_VERSION = 3          # include/sde.h: the signatures below are this version's
 SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
 SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2
@@ -73,8 +74,11 @@ SIGNATURES = {
     "sde_sgm_8path_wta_pair": (c_int, [c_void_p] * 8 + [c_int, c_int, c_int, c_int, c_void_p]),
     "sde_sgm_direction": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "sde_cbca_arms": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, ctypes.c_float, c_void_p, c_void_p]),
-    "sde_cbca": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p]),
-    "sde_cbca_pair": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
+    "sde_cbca_workspace_bytes": (ctypes.c_size_t, [c_int, c_int]),
+    "sde_cbca": (c_int, [c_void_p] * 4 + [c_int] * 6 + [c_void_p, ctypes.c_size_t, c_void_p]),
+    "sde_cbca_pair": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p, ctypes.c_size_t, c_void_p]),
+    "sde_cbca_lr": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, ctypes.c_size_t, c_void_p]),
+    "sde_cbca_reciprocals": (c_int, [c_void_p, c_int, c_void_p]),
     "sde_lr_check": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_lrc_fill": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sde_median5": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
@@ -109,6 +113,10 @@ def _load():
         fn.argtypes = args
     if missing:
         raise ImportError(f"{LIB} does not export {missing}")
+    # a library of another ABI would take these argument lists with other meanings (e.g. ABI 3 added
+    # the aggregation workspace): refuse it rather than pass it the wrong arguments
+    if lib.sde_abi_version() != SDE_ABI_VERSION:
+        raise ImportError(f"{LIB} has ABI {lib.sde_abi_version()}, this binding needs {SDE_ABI_VERSION}: rebuild it")
     return lib
 
 

@@ -2,24 +2,34 @@
 //
 // BUILD-DEFINED stage: the reference has no CBCA (only the
 // buffer name d_cost_volumel_after_aggr, process_functional.py:268,347, and an
-// unused timer label, match.py:98).  The definition -- cross arms on intensity
-// + distance, support intersected with the other image's arms at x -/+ d,
-// horizontal-then-vertical sums, mean over the support, N iterations -- is
-// stated once in the CPU restatement under oracle/ (test infrastructure); these
-// kernels reproduce it bit for bit (fp32 sums in ascending offset order from
-// 0.0f, exact integer counts, one IEEE division).
+// unused timer label, match.py:98).  The definition (v2, round 4) is stated once
+// in the CPU restatement under oracle/ (test infrastructure); these kernels
+// reproduce it bit for bit:
+//  - every volume is aggregated in LEFT coordinates; a voxel is valid iff its
+//    right-image pixel q - d is inside the image, and invalid voxels pass through;
+//  - support arms = min(left-image arm at q, right-image arm at q - d), so the
+//    right-referenced volume's aggregation is the shear of the left one's: the GPU
+//    path aggregates ONE volume and writes the other as its shear (sde_cbca_lr);
+//  - prefix chains (fp64, sequential) restart per segment of SDE_CBCA_SEG
+//    positions at kS - M (M = L1 - 1): any wave can take any segment after an
+//    M-position pre-roll, so the passes are persistent, load-balanced grids;
+//  - the mean multiplies by the correctly rounded fp64 reciprocal of the exact
+//    integer count (sde_cbca_reciprocals exposes the kernels' values).
 //
-// Mapping.  Both passes are line scans: one wave (one workgroup) walks one
-// line -- a row for the horizontal pass, a column for the vertical one -- for
-// one chunk of 64 disparities (lane = d, so each step moves one 256-B
-// contiguous run of the HWD volume).  The fp64 prefix sum P of the definition
-// is the wave's running state; the last 2R+2 prefixes live in a wave-private
-// LDS ring, so each output is two LDS reads at per-lane offsets (its own arms)
-// and one subtraction: O(1) work per voxel whatever the arm lengths.  The
-// output trails the front by R positions (its right/down arm is at most R).
-// Cost values and both images' arms are prefetched 8 positions ahead in a
-// register ring (unconditional, clamped loads), and the support arms of the
-// last R + 1 positions stay in registers for the trailing output.
+// Mapping (both passes): one wave per (line, 64-disparity chunk, segment) item,
+// lane = d, so each step moves one 256-B run of the HWD volume.  The chain P is the
+// wave's running state; the last 2R+2 prefixes live in a wave-private LDS ring, so
+// an output is two LDS reads at per-lane slots and one subtraction, trailing the
+// front by R >= M positions.  Per step the only vector-memory operations are the
+// cost load (prefetched a whole ring ahead, PF = 2R+2 positions: ~7 KB in flight
+// per wave) and the output store; the arms come in once per ring block:
+//  - horizontal pass: the left-image arms of the block's trailing positions are
+//    one dword per lane, read back with v_readlane; the right-image arm of lane i
+//    at position t is the value lane i-1 held at t-1, so it rides a DPP wave_shr:1
+//    chain fed at lane 0;
+//  - vertical pass: both images' arms come from a column-major copy in the
+//    workspace (sde_cbca_workspace_bytes), the right image's as one dwordx4 per
+//    lane per four rows.
 #include "sde_common.h"
 
 namespace sde {
@@ -47,16 +57,37 @@ __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict_
     arms[p] = packed;
 }
 
-// Cache policy of the cost stream (aux bit 1 = nt on gfx950): 1 loads, 2 stores.  The volumes are
-// streamed once per pass: nontemporal both ways, 1.513 -> 1.468 ms per pair iteration
-// (tools/lib_variants.py; the arms stay cached -- every line re-reads them).
+// Column-major copy of the arms, aT[x * Hp + y] (Hp = H rounded up to 4: a lane's dwordx4 of four
+// rows is 16-B aligned).  32 x 32 tiles through LDS.
+__global__ __launch_bounds__(256) void cbca_transpose_kernel(const uint32_t *__restrict__ a, uint32_t *__restrict__ aT,
+                                                             int H, int W, int Hp)
+{
+    __shared__ uint32_t t[32][33];
+    const int x0 = blockIdx.x * 32, y0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+        const int y = y0 + ty + i, x = x0 + tx;
+        t[ty + i][tx] = (y < H && x < W) ? a[(size_t)y * W + x] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+        const int x = x0 + ty + i, y = y0 + tx;
+        if (x < W && y < Hp) aT[(size_t)x * Hp + y] = t[tx][ty + i];
+    }
+}
+
+// Cache policy of the cost streams (aux bit 1 = nt on gfx950): each voxel is read once and written
+// once per pass (round 2: nontemporal both ways, 1.513 -> 1.468 ms per pair iteration).
 #ifndef CBCA_NT
 #define CBCA_NT 3
 #endif
+constexpr uint32_t CB_OOB = 0x80000000u;    // a voffset past every range: load 0, store dropped
 
-// Buffer descriptor (wave-uniform inputs only) for raw dword loads/stores with a 32-bit
-// per-lane voffset, an SGPR soffset and the hardware range check (voffset >= bytes -> 0 on
-// load, dropped on store).
+// Buffer descriptor (wave-uniform inputs only) for raw dword loads/stores with a 32-bit per-lane
+// voffset, an SGPR soffset and the hardware range check on voffset (>= bytes: load 0, store
+// dropped; every range below is < 2^31, so a voffset of CB_OOB is always out of range).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t cb_rsrc(const void *base, uint32_t bytes)
 {
     const uintptr_t b = (uintptr_t)base;
@@ -66,207 +97,470 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cb_rsrc(const void *base, uint
     return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// One launch covers up to two volumes (grid.z): the left- and right-referenced volumes of a pair
-// are independent, and one launch of both fills the machine in whole rounds of line-waves (a
-// 1024^2 x 192 pass has 3072 line-waves per volume against 2048-2560 resident: alone, its second
-// round runs half empty).
-#ifndef CBCA_PF
-#define CBCA_PF 16    // positions prefetched ahead (A/B builds: 8)
-#endif
-struct CbcaVolumes {
-    const float *src[2];
-    float *dst[2];
-    const uint32_t *ref[2], *oth[2];
-    int side[2];
-};
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// The scan of one line of one volume (SIDE compile-time: each launch holds both instantiations
-// and picks one per workgroup).
-template <int R, bool VERT, int SIDE>
-__device__ __forceinline__ void cbca_scan(const float *__restrict__ src, float *__restrict__ dst,
-                                          const uint32_t *__restrict__ ref, const uint32_t *__restrict__ oth,
-                                          int H, int W, int D, double *__restrict__ sP, uint16_t *__restrict__ sN)
+__device__ __forceinline__ uint32_t ruint(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+
+// (x + RS) mod RS for x in [-RS, RS): x + RS, then min_u32 with x + RS - RS (wraps huge when < 0)
+template <int RS>
+__device__ __forceinline__ uint32_t ring_slot(int x)
 {
-    constexpr int RS = 2 * R + 2;      // prefix ring: positions [f - 2R - 1, f]; also the unroll
-    constexpr int U = R + 1;           // support ring (trailing output reads the slot of f - R)
-    constexpr int PF = CBCA_PF;        // prefetch distance (vmcnt saturates at 63 outstanding ops)
-    static_assert((RS & (RS - 1)) == 0 && RS % U == 0 && RS % PF == 0, "ring sizes");
-    const int lane = threadIdx.x;
-    // Lanes past D work on d = D-1: they compute lane D-1's value and store it to the
-    // same address, so no load, LDS access or store in the scan is predicated.
-    const int d = min((int)blockIdx.x * 64 + lane, D - 1);
-    const int line = blockIdx.y;
-    const int len = VERT ? H : W;
-    // Addressing (all per-step offsets in SGPRs, per-lane parts fixed):
-    //  H pass (line = row y): cost/out buffers over the row, voffset 4d, soffset 4qD; reference
-    //   arms: voffset 0, soffset 4q; other arms: voffset 4(q -/+ d) -- outside the row it fails
-    //   the range check and reads 0, i.e. "no other pixel: support {p}".
-    //  V pass (line = column x): cost/out buffers rebased every RS rows (a column spans
-    //   H*W*D*4 bytes, beyond 32-bit offsets), voffset 4d, soffset 4(q - q0)WD; arms: voffset 0 /
-    //   4(x -/+ d) (masked when outside the row), soffset 4qW.
-    const uint32_t d4 = 4u * d;
-    // opaque per-lane zero for the (wave-uniform) reference-arm loads: keeps their value a VGPR,
-    // so no readfirstlane (and no wait for it) lands on every step
-    const uint32_t vz = __builtin_amdgcn_mbcnt_lo(0u, 0u);
-    const int ov = SIDE == SDE_SIDE_LEFT ? line - d : line + d;
-    const bool vok = ov >= 0 && ov < W;
-    const uint32_t ov4 = 4u * (uint32_t)(vok ? ov : 0);
-    const uint32_t linebytes = 4u * (uint32_t)W * (uint32_t)D;       // one row of the volume
-    __amdgpu_buffer_rsrc_t rc, rd;
-    __amdgpu_buffer_rsrc_t ra = cb_rsrc(ref + (VERT ? (size_t)line : (size_t)line * W), VERT ? 0xffffffffu : 4u * W);
-    __amdgpu_buffer_rsrc_t rb = cb_rsrc(oth + (VERT ? 0 : (size_t)line * W), VERT ? 0xffffffffu : 4u * W);
-    if (!VERT) {
-        rc = cb_rsrc(src + (size_t)line * W * D, linebytes);
-        rd = cb_rsrc(dst + (size_t)line * W * D, linebytes);
-    }
-
-    double P_acc = 0.0;
-    uint32_t N_acc = 0;
-    float cr[PF];
-    uint32_t ar[PF], br[PF];
-    uint32_t sup[U];    // VERT: (up | down << 8) of the last U positions; else (left | right << 8)
-    // q: position (clamped by the caller in the tail); qb: the V pass's current rebase row
-    auto issue = [&](int q, int qb, int slot) {
-        if (VERT) {
-            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                     rc, d4, (int)((uint32_t)(q - qb) * linebytes), CBCA_NT & 1 ? 2 : 0));
-            ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q * W, 0);
-            br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, ov4, 4 * q * W, 0);
-        } else {
-            cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, d4, 4 * q * D, CBCA_NT & 1 ? 2 : 0));
-            ar[slot] = __builtin_amdgcn_raw_buffer_load_b32(ra, vz, 4 * q, 0);
-            uint32_t o4 = SIDE == SDE_SIDE_LEFT ? 4u * (uint32_t)q - d4 : 4u * (uint32_t)q + d4;
-            // opaque: the whole offset must reach the range check as voffset.  Left to itself the
-            // compiler moves the step's constant part of q into the instruction offset, and a
-            // voffset that wrapped below zero (x - d < 0 at the block start, >= 0 at this step)
-            // then fails the check and reads 0 for a pixel inside the row.
-            asm volatile("" : "+v"(o4));
-            br[slot] = __builtin_amdgcn_raw_buffer_load_b32(rb, o4, 0, 0);
-        }
-    };
-    auto step = [&](int j, int f, int qb, bool tail) {
-        const int slot = j % PF;
-        const uint32_t a = ar[slot];
-        uint32_t b = br[slot];
-        if (VERT) b = vok ? b : 0u;                 // no other pixel: support {p}
-        const int l = min(a & 255, b & 255), r = min((a >> 8) & 255, (b >> 8) & 255);
-        // front: position f (tail positions >= len re-read the last one; never referenced)
-        P_acc += (double)cr[slot];
-        sP[j * 64 + lane] = P_acc;
-        if (VERT) {
-            N_acc += (uint32_t)(l + r + 1);
-            sN[j * 64 + lane] = (uint16_t)N_acc;
-            sup[j % U] = min((a >> 16) & 255, (b >> 16) & 255) | (min(a >> 24, b >> 24) << 8);
-        } else {
-            sup[j % U] = (uint32_t)l | ((uint32_t)r << 8);
-        }
-        const int qn = tail ? min(f + PF, len - 1) : f + PF;
-        issue(qn, qb, slot);
-        // trailing output y = f - R; its support arms from the ring slot of position y
-        const int y = f - R;
-        if (y >= 0 && (!tail || y < len)) {
-            const uint32_t sy = sup[(j + 1) % U];
-            const int lo = sy & 255, hi = sy >> 8;
-            const int ib = ((j - R + hi) & (RS - 1)) * 64 + lane, ia = ((j - R - lo - 1) & (RS - 1)) * 64 + lane;
-            const double pb = sP[ib], pa = sP[ia];
-            float out;
-            if (VERT) out = (float)((pb - pa) / (double)(uint16_t)(sN[ib] - sN[ia]));
-            else out = (float)(pb - pa);
-            const int so = VERT ? (int)((uint32_t)(y - qb) * linebytes) : 4 * y * D;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, d4, so, CBCA_NT & 2 ? 2 : 0);
-        }
-    };
-    // V pass: (re)base the cost / output descriptors on row qb; soffsets then stay below
-    // (2 RS + PF) rows of the volume
-    auto rebase = [&](int qb) {
-        if (VERT) {
-            const size_t off = (size_t)qb * W * D + (size_t)line * D;
-            rc = cb_rsrc(src + off, 0xffffffffu);
-            rd = cb_rsrc(dst + off, 0xffffffffu);
-        }
-    };
-    // V pass: the descriptors are rebased on row qb = f0 - R at every block start, so a block's
-    // outputs (rows f0 - R ..) and loads (rows up to f0 + RS + PF) sit at small soffsets; loads
-    // already in flight keep the addresses they were issued with.
-    rebase(-R);
-#pragma unroll
-    for (int j = 0; j < PF; j++) issue(min(j, len - 1), -R, j);
-#pragma unroll
-    for (int j = 0; j < U; j++) sup[j] = 0u;
-    sP[(RS - 1) * 64 + lane] = 0.0;        // P(-1) = 0 (slot of position -1; rewritten at f = RS-1)
-    if (VERT) sN[(RS - 1) * 64 + lane] = 0;
-    int f0 = 0;
-    // main blocks: every prefetched position is inside the line (no clamps)
-    for (; f0 + RS + PF <= len; f0 += RS) {
-        const int qb = f0 - R;
-        rebase(qb);
-#pragma unroll
-        for (int j = 0; j < RS; j++) step(j, f0 + j, qb, false);
-    }
-    for (; f0 < len + R; f0 += RS) {
-        const int qb = f0 - R;
-        rebase(qb);
-#pragma unroll
-        for (int j = 0; j < RS; j++) step(j, f0 + j, qb, true);
-    }
+    const uint32_t u = (uint32_t)(x + RS);
+    return min(u, u - (uint32_t)RS);
 }
 
-template <int R, bool VERT>
-__global__ __launch_bounds__(64) void cbca_scan_kernel(const CbcaVolumes vols, int H, int W, int D)
+// Correctly rounded 1/c for the exact support counts (1 <= c <= (2*31+1)^2): v_rcp_f64 and two
+// Newton steps; sde_cbca_reciprocals returns these values (the tests compare them with the IEEE
+// quotient for every count).
+__device__ __forceinline__ double cb_recip(uint32_t c)
 {
-    constexpr int RS = 2 * R + 2;
-    __shared__ double sP[RS * 64];
-    // support-count prefixes mod 2^16: a support holds at most (2R+1)^2 < 2^16 pixels, so the
-    // difference of two ring entries taken mod 2^16 is the exact count (half the LDS of int32:
-    // more line-waves per CU)
-    static_assert((2 * R + 1) * (2 * R + 1) < 65536, "support counts must fit 16 bits");
-    __shared__ uint16_t sN[VERT ? RS * 64 : 1];
-    const int z = blockIdx.z;
-    if (vols.side[z] == SDE_SIDE_LEFT)
-        cbca_scan<R, VERT, SDE_SIDE_LEFT>(vols.src[z], vols.dst[z], vols.ref[z], vols.oth[z], H, W, D, sP, sN);
-    else
-        cbca_scan<R, VERT, SDE_SIDE_RIGHT>(vols.src[z], vols.dst[z], vols.ref[z], vols.oth[z], H, W, D, sP, sN);
+    const double cd = (double)c;
+    double r = __builtin_amdgcn_rcp(cd);
+    double e = __builtin_fma(-cd, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-cd, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+struct CbcaArgs {
+    const float *src;
+    float *dst;
+    const uint32_t *al, *ar;       // row-major arms (left / right image): horizontal pass
+    const uint32_t *alT, *arT;     // column-major arms (pitch Hp): vertical pass
+    int H, W, D, M, Hp;
+    int nseg, ndc;
+    int64_t nitems;
+    int per;                       // items per wave (contiguous range)
+    int64_t chunk_first[9];        // vertical pass: first item of chunk c (valid columns only)
+};
+
+// ---------------------------------------------------------------------------------------------
+// Horizontal pass: item = (row y, chunk c, segment k), k fastest, so a wave's consecutive items
+// are consecutive segments of one row.
+// ---------------------------------------------------------------------------------------------
+// Opaque to the optimiser: keeps a per-step offset an incremented register instead of 2R+2
+// block-invariant constants hoisted out of the loop (SGPR pressure, spills, drained prefetch).
+__device__ __forceinline__ uint32_t opq_s(uint32_t v)
+{
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t opq_v(uint32_t v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 template <int R>
-static void cbca_iters(const CbcaVolumes &fwd, const CbcaVolumes &bwd, int nvol, int H, int W, int D, int iters,
-                       hipStream_t st)
+__device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int k, double *__restrict__ sP)
 {
-    const int ndc = (D + 63) / 64;
-    for (int it = 0; it < iters; it++) {
-        cbca_scan_kernel<R, false><<<dim3(ndc, H, nvol), 64, 0, st>>>(fwd, H, W, D);
-        cbca_scan_kernel<R, true><<<dim3(ndc, W, nvol), 64, 0, st>>>(bwd, H, W, D);
+    constexpr int RS = 2 * R + 2, PF = RS;
+    const int lane = threadIdx.x;
+    const int W = A.W, D = A.D, M = A.M;
+    const int d0 = 64 * c, d = d0 + lane;
+    const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, W);
+    if (t1 <= d0) return;                          // every voxel of the segment is invalid
+    const int fs = max(t0 - M, d0);                // walk start = lane 0's chain base
+    const int fe = t1 - 1 + R;                     // last front position (output t1 - 1)
+    const uint32_t D4 = 4u * (uint32_t)D;
+    const uint32_t dl4 = 4u * (uint32_t)min(d, D - 1);
+    const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
+    const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + (size_t)y * W * D, rowbytes);
+    const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + (size_t)y * W * D, rowbytes);
+    const __amdgpu_buffer_rsrc_t ra = cb_rsrc(A.al + (size_t)y * W, 4u * W);
+    const __amdgpu_buffer_rsrc_t rb = cb_rsrc(A.ar + (size_t)y * W, 4u * W);
+    // a lane stores output t iff t >= th = max(t0, d) (valid voxel of this segment) and d < D
+    const int th = d < D ? max(t0, d) : 0x7FFFFFFF;
+
+    float cr[PF];
+    // block arms: lane j (< RS) holds the left-image arm at the block's trailing position tb + j and
+    // the right-image arm at tb + j - d0 (outside the row: 0, only ever used by invalid lanes)
+    auto arms_blk = [&](int tb, uint32_t &av, uint32_t &bv) {
+        av = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(tb + lane), 0, 0);
+        bv = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(tb + lane - d0), 0, 0);
+    };
+#pragma unroll
+    for (int j = 0; j < PF; j++)
+        cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)(D4 * (uint32_t)min(fs + j, W - 1)),
+                                                                               CBCA_NT & 1 ? 2 : 0));
+    uint32_t Ab, Bb, An, Bn;
+    arms_blk(fs - R, Ab, Bb);
+    // right-image arm of the trailing position, lane i = pixel t - d0 - i: the state before step fs
+    uint32_t X = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(fs - R - 1 - d0 - lane), 0, 0);
+    double P = 0.0;
+    sP[(RS - 1) * 64 + lane] = 0.0;               // P(fs - 1) = 0: read before position fs + RS - 1 lands
+    // per-lane store offset of output t (4d + 4tD), advanced every step
+    uint32_t vst = 4u * (uint32_t)d + D4 * (uint32_t)(fs - R);
+
+    // step j of a block at front f; CLAMP: prefetch positions may pass the row end (tail blocks)
+    auto step = [&](int j, int f, uint32_t &sld, bool clamp) {
+        const int slot = j % PF;
+        // front: the chain of this lane starts at max(t0 - M, d) >= fs
+        const float cv = cr[slot];
+        P += f >= d ? (double)cv : 0.0;
+        sP[j * 64 + lane] = P;
+        const uint32_t so = clamp ? D4 * (uint32_t)min(f + PF, W - 1) : sld;
+        cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
+        sld = opq_s(sld + D4);
+        // trailing output t = f - R: left-image arm (uniform) and the right-image arm chain
+        const int t = f - R;
+        const uint32_t a = ruint(Ab, j);
+        const uint32_t nb = ruint(Bb, j);
+        X = (uint32_t)__builtin_amdgcn_update_dpp((int)nb, (int)X, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- nb
+        const int hl = min(a & 255u, X & 255u), hr = min((a >> 8) & 255u, (X >> 8) & 255u);
+        const uint32_t ib = ring_slot<RS>(j - R + hr), ia = ring_slot<RS>(j - R - hl - 1);
+        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        const float out = (float)(pb - pa);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, t >= th ? vst : CB_OOB, 0,
+                                              CBCA_NT & 2 ? 2 : 0);
+        vst = opq_v(vst + D4);
+    };
+    int fb = fs;
+    // main blocks: every front and prefetch position inside the row
+    for (; fb + RS - 1 <= fe && fb + RS - 1 + PF <= W - 1; fb += RS) {
+        arms_blk(fb + RS - R, An, Bn);
+        uint32_t sld = D4 * (uint32_t)(fb + PF);
+#pragma unroll
+        for (int j = 0; j < RS; j++) step(j, fb + j, sld, false);
+        Ab = An;
+        Bb = Bn;
+    }
+    for (; fb <= fe; fb += RS) {
+        arms_blk(fb + RS - R, An, Bn);
+        uint32_t sld = 0;
+#pragma unroll
+        for (int j = 0; j < RS; j++)
+            if (fb + j <= fe) step(j, fb + j, sld, true);
+        Ab = An;
+        Bb = Bn;
     }
 }
 
-// The scans address with 32-bit buffer offsets (signed soffsets): the H pass reaches 4*W*D bytes
-// into a row and the V pass (q - qb) <= 3R + 17 rows of 4*W*D bytes past its rebase row (loads
-// prefetched PF = 16 positions ahead of a 2R+2 block that starts R rows after qb); the V pass's
-// arm loads reach 4*H*W bytes.  Beyond that an offset would wrap silently (the column
-// descriptors carry no range limit), so such shapes are refused.
+template <int R>
+__global__ __launch_bounds__(64, 3) void cbca_h_kernel(const CbcaArgs A)
+{
+    __shared__ double sP[(2 * R + 2) * 64];
+    const int64_t i0 = (int64_t)blockIdx.x * A.per, i1 = min(i0 + A.per, A.nitems);
+    for (int64_t it = i0; it < i1; it++) {
+        const int k = (int)(it % A.nseg);
+        const int64_t r = it / A.nseg;
+        cbca_h_item<R>(A, (int)(r / A.ndc), (int)(r % A.ndc), k, sP);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Vertical pass: item = (chunk c, column x >= 64c, segment k), k fastest; only columns with at
+// least one valid lane (x >= d0) are items.
+// ---------------------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, double *__restrict__ sP,
+                                            uint16_t *__restrict__ sN)
+{
+    constexpr int RS = 2 * R + 2, PF = RS, U = R + 1, NQ = RS / 4;
+    static_assert(RS % 4 == 0 && RS % U == 0, "ring sizes");
+    const int lane = threadIdx.x;
+    const int H = A.H, W = A.W, D = A.D, M = A.M, Hp = A.Hp;
+    const int d0 = 64 * c, d = d0 + lane;
+    const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, H);
+    const int fc = max(t0 - M, 0);               // chain base (every valid lane)
+    const int fs = fc & ~3;                      // walk start: 16-B aligned dwordx4 of four rows
+    const int fe = t1 - 1 + R;
+    const bool lane_ok = d < D && d <= x;
+    const uint32_t dl4 = 4u * (uint32_t)min(d, D - 1);
+    const uint32_t rowv = 4u * (uint32_t)W * (uint32_t)D;       // one row of the volume
+    // descriptors over the column, rebased on row fbase (loads) / fb - R (stores) every block, their
+    // ranges covering the rows a block touches (< 2^31 bytes: the shape check)
+    const uint32_t win = (uint32_t)(RS + PF + R + 1) * rowv;
+    const __amdgpu_buffer_rsrc_t ra = cb_rsrc(A.alT + (size_t)x * Hp, 4u * (uint32_t)Hp);
+    const __amdgpu_buffer_rsrc_t rb = cb_rsrc(A.arT, 4u * (uint32_t)W * (uint32_t)Hp);
+    const uint32_t bcol = lane_ok ? 4u * (uint32_t)(x - d) * (uint32_t)Hp : CB_OOB;
+
+    float cr[PF];
+    u32x4 Bq[NQ];                // right-image arms of rows fb + 4m .. +3 (per lane); Bq[m] is
+                                 // reloaded with the next block's rows once its last row is used
+    uint32_t Ab, An;             // left-image arm of row fb + lane (lanes < RS)
+    uint32_t sup[U];             // (vu | vd << 16) of the last U front positions
+    auto arm_q = [&](int row) {  // rows row .. row + 3 of the right image at x - d
+        const uint32_t off = bcol == CB_OOB ? CB_OOB : bcol + 4u * (uint32_t)row;
+        return __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
+    };
+    {
+        const __amdgpu_buffer_rsrc_t rc0 = cb_rsrc(A.src + ((size_t)fs * W + x) * D, win);
+#pragma unroll
+        for (int j = 0; j < PF; j++)
+            cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rc0, dl4, (int)(rowv * (uint32_t)(min(fs + j, H - 1) - fs)), CBCA_NT & 1 ? 2 : 0));
+    }
+    Ab = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + lane), 0, 0);
+#pragma unroll
+    for (int m = 0; m < NQ; m++) Bq[m] = arm_q(fs + 4 * m);
+#pragma unroll
+    for (int j = 0; j < U; j++) sup[j] = 0u;
+    double P = 0.0;
+    uint32_t N = 0;
+    sP[(RS - 1) * 64 + lane] = 0.0;               // Q(fs - 1) = 0, N(fs - 1) = 0
+    sN[(RS - 1) * 64 + lane] = 0;
+
+    // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R
+    auto step = [&](int j, int f, int fbase, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rd, uint32_t &sld,
+                    uint32_t &sst, bool clamp) {
+        const int slot = j % PF;
+        // front f: chain (rows >= fc), count contribution and vertical support
+        const uint32_t a = ruint(Ab, j);
+        const uint32_t bw = Bq[j / 4][j % 4];
+        const uint32_t a02 = a & 0x00FF00FFu, a13 = (a >> 8) & 0x00FF00FFu;
+        const uint32_t b02 = bw & 0x00FF00FFu, b13 = (bw >> 8) & 0x00FF00FFu;
+        // per 16-bit half: (min l, min u) and (min r, min d)
+        const uint32_t m02 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a02),
+                                                                                    __builtin_bit_cast(u16x2, b02)));
+        const uint32_t m13 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a13),
+                                                                                    __builtin_bit_cast(u16x2, b13)));
+        const bool on = f >= fc;
+        P += on ? (double)cr[slot] : 0.0;
+        N += on ? ((m02 + m13) & 0xFFFFu) + 1u : 0u;
+        sP[j * 64 + lane] = P;
+        sN[j * 64 + lane] = (uint16_t)N;
+        sup[j % U] = (m02 >> 16) | (m13 & 0xFFFF0000u);
+        if (j % 4 == 3) Bq[j / 4] = arm_q(f + RS - 3);      // the next block's rows f + RS - 3 ..
+        const uint32_t so = clamp ? rowv * (uint32_t)(min(f + PF, H - 1) - fbase) : sld;
+        cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
+        sld = opq_s(sld + rowv);
+        // trailing output t = f - R, support from the ring slot of position t
+        const int t = f - R;
+        const uint32_t sy = sup[(j + 1) % U];
+        const int vu = sy & 0xFFFF, vd = sy >> 16;
+        const uint32_t ib = ring_slot<RS>(j - R + vd), ia = ring_slot<RS>(j - R - vu - 1);
+        const double num = sP[ib * 64 + lane] - sP[ia * 64 + lane];
+        const uint32_t cnt = (uint16_t)(sN[ib * 64 + lane] - sN[ia * 64 + lane]);
+        const float out = (float)(num * cb_recip(cnt));
+        const uint32_t vo = (lane_ok && t >= t0) ? 4u * (uint32_t)d : CB_OOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, vo, (int)sst, CBCA_NT & 2 ? 2 : 0);
+        sst = opq_s(sst + rowv);
+    };
+    int fb = fs;
+    for (; fb + RS - 1 <= fe && fb + RS - 1 + PF <= H - 1; fb += RS) {
+        An = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + RS + lane), 0, 0);
+        // loads for positions fb + PF .. go against a descriptor rebased on row fb
+        const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fb * W + x) * D, win);
+        const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R) * W + x) * D, win);
+        uint32_t sld = rowv * (uint32_t)PF, sst = 0;
+#pragma unroll
+        for (int j = 0; j < RS; j++) step(j, fb + j, fb, rc, rd, sld, sst, false);
+        Ab = An;
+    }
+    for (; fb <= fe; fb += RS) {
+        An = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + RS + lane), 0, 0);
+        const int fbase = min(fb, H - 1);       // a tail block may start past the last row
+        const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fbase * W + x) * D, win);
+        const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R) * W + x) * D, win);
+        uint32_t sld = 0, sst = 0;
+#pragma unroll
+        for (int j = 0; j < RS; j++)
+            if (fb + j <= fe) step(j, fb + j, fbase, rc, rd, sld, sst, true);
+        Ab = An;
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(64, 3) void cbca_v_kernel(const CbcaArgs A)
+{
+    __shared__ double sP[(2 * R + 2) * 64];
+    __shared__ uint16_t sN[(2 * R + 2) * 64];
+    const int64_t i0 = (int64_t)blockIdx.x * A.per, i1 = min(i0 + A.per, A.nitems);
+    for (int64_t it = i0; it < i1; it++) {
+        int c = 0;
+        while (c + 1 < A.ndc && it >= A.chunk_first[c + 1]) c++;
+        const int64_t r = it - A.chunk_first[c];
+        const int k = (int)(r % A.nseg);
+        cbca_v_item<R>(A, 64 * c + (int)(r / A.nseg), c, k, sP, sN);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-disparity rotation of the rows: out(y, x, d) = in(y, (x + s*d) mod W, d).  s = +1 with
+// VALID_ONLY: the shear of an aggregated left volume into the right one's valid voxels (x + d <
+// W; the others untouched); s = -1 / +1 over every voxel: a right-referenced volume into left
+// coordinates and back (its invalid voxels ride on the left-coordinate invalid ones).
+// Tile = (row, 64-disparity chunk, 64 output pixels); its 127 source pixels are staged in LDS
+// (stride 64 floats: the diagonal reads hit 64 distinct banks), tiles sharing source pixels
+// sit 8 blocks apart (one XCD under round-robin dispatch: L2 reuse, speed only).
+// ---------------------------------------------------------------------------------------------
+template <bool VEC4>
+__global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restrict__ in, float *__restrict__ out, int H,
+                                                          int W, int D, int s, int valid_only, int64_t ntiles,
+                                                          int64_t per_xcd)
+{
+    __shared__ float buf[127 * 64];
+    const int64_t b = blockIdx.x;
+    const int64_t tile = (b % 8) * per_xcd + b / 8;
+    if (tile >= ntiles) return;
+    const int nxs = (W + 63) / 64, ndc = (D + 63) / 64;
+    const int xs = (int)(tile % nxs);
+    const int64_t rem = tile / nxs;
+    const int c = (int)(rem % ndc), y = (int)(rem / ndc);
+    const int x0 = 64 * xs, d0 = 64 * c;
+    const int tid = threadIdx.x;
+    const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
+    const __amdgpu_buffer_rsrc_t ri = cb_rsrc(in + (size_t)y * W * D, rowbytes);
+    const __amdgpu_buffer_rsrc_t ro = cb_rsrc(out + (size_t)y * W * D, rowbytes);
+    // source row r of the tile = pixel (base + r) mod W
+    const int64_t base = s > 0 ? (int64_t)x0 + d0 : (int64_t)x0 - d0 - 63;
+    auto srcpix = [&](int r) { return (int)((((base + r) % W) + W) % W); };
+    if (VEC4) {
+        // 16 lanes per 256-B run: thread t loads chunk t % 16 of rows t / 16 + 16 m
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+            const int r = tid / 16 + 16 * m;
+            if (r < 127) {
+                const int col = 4 * (tid % 16);
+                const uint32_t off = d0 + col < D ? 4u * ((uint32_t)srcpix(r) * D + d0 + col) : CB_OOB;
+                const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 0));
+                *(float4 *)&buf[r * 64 + col] = v;
+            }
+        }
+    } else {
+#pragma unroll 4
+        for (int m = 0; m < 32; m++) {
+            const int r = tid / 64 + 4 * m;
+            if (r < 127) {
+                const int col = tid % 64;
+                const uint32_t off = d0 + col < D ? 4u * ((uint32_t)srcpix(r) * D + d0 + col) : CB_OOB;
+                buf[r * 64 + col] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, off, 0, 0));
+            }
+        }
+    }
+    __syncthreads();
+    const int i = tid % 64, wv = tid / 64;
+    const int d = d0 + i;
+#pragma unroll 4
+    for (int p = wv; p < 64; p += 4) {
+        const int x = x0 + p;
+        const int r = s > 0 ? p + i : p - i + 63;
+        const bool ok = x < W && d < D && (!valid_only || x + d < W);
+        const uint32_t off = ok ? 4u * ((uint32_t)x * D + d) : CB_OOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, buf[r * 64 + i]), ro, off, 0, 0);
+    }
+}
+
+__global__ void cbca_recip_kernel(double *out, int n)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = cb_recip((uint32_t)(i + 1));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------------
+static inline int cb_hp(int H) { return (H + 3) & ~3; }
+
+static size_t cbca_ws_bytes(int H, int W) { return 2 * sizeof(uint32_t) * (size_t)cb_hp(H) * (size_t)W; }
+
+// Resident one-wave workgroups of a pass kernel (occupancy x CUs), per device and kernel.
+template <typename K>
+static int cb_resident(K kernel)
+{
+    int dev = 0, cus = 256, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, 0) != hipSuccess || per <= 0) per = 8;
+    return per * cus;
+}
+
+// Balanced static schedule: the fewest items per wave that fit the resident waves, then only as
+// many waves as that needs (every wave gets the same count, so none idles while others finish).
+static void cb_schedule(CbcaArgs &A, int resident, int &grid)
+{
+    const int64_t per = (A.nitems + resident - 1) / resident;
+    A.per = (int)(per > 0 ? per : 1);
+    grid = (int)((A.nitems + A.per - 1) / A.per);
+}
+
+// One left-coordinate volume: iters x (horizontal src -> tmp, vertical tmp -> src), in place.
+template <int R>
+static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uint32_t *ar, const uint32_t *alT,
+                            const uint32_t *arT, int H, int W, int D, int L1, int iters, hipStream_t st)
+{
+    CbcaArgs h{};
+    h.al = al, h.ar = ar, h.alT = alT, h.arT = arT;
+    h.H = H, h.W = W, h.D = D, h.M = L1 - 1, h.Hp = cb_hp(H);
+    h.ndc = (D + 63) / 64;
+    CbcaArgs v = h;
+    h.nseg = (W + SDE_CBCA_SEG - 1) / SDE_CBCA_SEG;
+    h.nitems = (int64_t)H * h.ndc * h.nseg;
+    v.nseg = (H + SDE_CBCA_SEG - 1) / SDE_CBCA_SEG;
+    int64_t n = 0;
+    for (int c = 0; c < v.ndc; c++) {
+        v.chunk_first[c] = n;
+        n += (int64_t)max(W - 64 * c, 0) * v.nseg;
+    }
+    v.chunk_first[v.ndc] = n;
+    v.nitems = n;
+    static std::atomic<int> res_h{0}, res_v{0};
+    if (!res_h.load()) res_h = cb_resident(cbca_h_kernel<R>);
+    if (!res_v.load()) res_v = cb_resident(cbca_v_kernel<R>);
+    int gh = 0, gv = 0;
+    cb_schedule(h, res_h.load(), gh);
+    cb_schedule(v, res_v.load(), gv);
+    h.src = cv, h.dst = tmp;
+    v.src = tmp, v.dst = cv;
+    for (int it = 0; it < iters; it++) {
+        if (h.nitems > 0) cbca_h_kernel<R><<<gh, 64, 0, st>>>(h);
+        if (v.nitems > 0) cbca_v_kernel<R><<<gv, 64, 0, st>>>(v);
+    }
+}
+
+static void cbca_rotate(const float *in, float *out, int H, int W, int D, int s, bool valid_only, hipStream_t st)
+{
+    const int64_t ntiles = (int64_t)H * ((D + 63) / 64) * ((W + 63) / 64);
+    const int64_t per = (ntiles + 7) / 8;
+    const int64_t grid = 8 * per;
+    if (D % 4 == 0)
+        cbca_rotate_kernel<true><<<(unsigned)grid, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles, per);
+    else
+        cbca_rotate_kernel<false><<<(unsigned)grid, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles, per);
+}
+
+// Shapes the 32-bit offsets cover (refused with SDE_ERR_ARG otherwise): a row of the volume and a
+// vertical-pass block window ((RS + PF + R + 1) rows, RS = PF = 2R + 2) below 2^31 bytes, the
+// arms (and their column-major copy) below 2^31 bytes, at most 8 disparity chunks (D <= 512).
+static int cbca_r(int L1) { return L1 <= 14 ? 13 : L1 <= 16 ? 15 : 31; }
 static bool cbca_shape_ok(int H, int W, int D, int L1)
 {
-    if (H > 65535 || W > 65535) return false;            // grid.y = lines
-    const int R = L1 <= 16 ? 15 : 31;
+    if (H <= 0 || W <= 0 || D <= 0 || D > 512 || L1 < 1 || L1 > SDE_CBCA_MAX_L1) return false;
+    const int R = cbca_r(L1);
     const int64_t row = 4 * (int64_t)W * D;
-    return (3 * R + 18) * row < ((int64_t)1 << 31) && 4 * (int64_t)H * W < ((int64_t)1 << 31);
+    return (int64_t)(5 * R + 5) * row < ((int64_t)1 << 31) && 4 * (int64_t)cb_hp(H) * W < ((int64_t)1 << 31) &&
+           (int64_t)H * ((D + 63) / 64) * ((W + 63) / 64) < ((int64_t)1 << 31) - 8;
 }
 
-// fwd: horizontal pass cv -> tmp; bwd: vertical pass tmp -> cv
-static int cbca_launch(float *const cv[2], float *const tmp[2], const uint32_t *const ref[2],
-                       const uint32_t *const oth[2], const int side[2], int nvol, int H, int W, int D, int L1,
-                       int iters, hipStream_t st)
+static int cbca_left(float *cv, float *tmp, const uint32_t *al, const uint32_t *ar, int H, int W, int D, int L1,
+                     int iters, void *ws, hipStream_t st)
 {
-    CbcaVolumes fwd{}, bwd{};
-    for (int k = 0; k < nvol; k++) {
-        fwd.src[k] = cv[k], fwd.dst[k] = tmp[k];
-        bwd.src[k] = tmp[k], bwd.dst[k] = cv[k];
-        fwd.ref[k] = bwd.ref[k] = ref[k];
-        fwd.oth[k] = bwd.oth[k] = oth[k];
-        fwd.side[k] = bwd.side[k] = side[k];
+    if (iters == 0) return SDE_OK;
+    const int Hp = cb_hp(H);
+    uint32_t *alT = (uint32_t *)ws, *arT = alT + (size_t)Hp * W;
+    const dim3 tg((W + 31) / 32, (Hp + 31) / 32);
+    cbca_transpose_kernel<<<tg, 256, 0, st>>>(al, alT, H, W, Hp);
+    cbca_transpose_kernel<<<tg, 256, 0, st>>>(ar, arT, H, W, Hp);
+    switch (cbca_r(L1)) {
+    case 13: cbca_left_iters<13>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
+    case 15: cbca_left_iters<15>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
+    default: cbca_left_iters<31>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
     }
-    if (L1 <= 16) cbca_iters<15>(fwd, bwd, nvol, H, W, D, iters, st);
-    else cbca_iters<31>(fwd, bwd, nvol, H, W, D, iters, st);
+    return launch_status();
+}
+
+// A right-referenced volume: rotated into left coordinates in tmp, aggregated there with cv as the
+// scratch, rotated back.  al / ar: the left / right image's arms.
+static int cbca_right(float *cv, float *tmp, const uint32_t *al, const uint32_t *ar, int H, int W, int D, int L1,
+                      int iters, void *ws, hipStream_t st)
+{
+    if (iters == 0) return SDE_OK;
+    cbca_rotate(cv, tmp, H, W, D, -1, false, st);
+    const int s = cbca_left(tmp, cv, al, ar, H, W, D, L1, iters, ws, st);
+    if (s != SDE_OK) return s;
+    cbca_rotate(tmp, cv, H, W, D, +1, false, st);
     return launch_status();
 }
 
@@ -282,33 +576,55 @@ SDE_EXPORT int sde_cbca_arms(const float *img, int64_t pitch, int H, int W, int 
     return launch_status();
 }
 
-SDE_EXPORT int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W,
-                        int D, int side, int L1, int iters, void *stream)
+SDE_EXPORT size_t sde_cbca_workspace_bytes(int H, int W)
 {
-    if (!cv || !tmp || !arms_ref || !arms_other || H <= 0 || W <= 0 || D <= 0 || iters < 0 || L1 < 1 ||
-        L1 > SDE_CBCA_MAX_L1 || (side != SDE_SIDE_LEFT && side != SDE_SIDE_RIGHT) || cv == tmp)
+    if (H <= 0 || W <= 0) return 0;
+    return cbca_ws_bytes(H, W);
+}
+
+SDE_EXPORT int sde_cbca(float *cv, float *tmp, const uint32_t *arms_ref, const uint32_t *arms_other, int H, int W,
+                        int D, int side, int L1, int iters, void *ws, size_t ws_bytes, void *stream)
+{
+    if (!cv || !tmp || !arms_ref || !arms_other || iters < 0 || (side != SDE_SIDE_LEFT && side != SDE_SIDE_RIGHT) ||
+        cv == tmp || !cbca_shape_ok(H, W, D, L1) || (iters > 0 && (!ws || ws_bytes < cbca_ws_bytes(H, W))))
         return SDE_ERR_ARG;
-    if (!cbca_shape_ok(H, W, D, L1)) return SDE_ERR_ARG;
-    float *const cvs[2] = {cv, nullptr}, *const tmps[2] = {tmp, nullptr};
-    const uint32_t *const refs[2] = {arms_ref, nullptr}, *const oths[2] = {arms_other, nullptr};
-    const int sides[2] = {side, side};
-    return cbca_launch(cvs, tmps, refs, oths, sides, 1, H, W, D, L1, iters, as_stream(stream));
+    if (side == SDE_SIDE_LEFT)
+        return cbca_left(cv, tmp, arms_ref, arms_other, H, W, D, L1, iters, ws, as_stream(stream));
+    return cbca_right(cv, tmp, arms_other, arms_ref, H, W, D, L1, iters, ws, as_stream(stream));
 }
 
 SDE_EXPORT int sde_cbca_pair(float *cv_l, float *tmp_l, float *cv_r, float *tmp_r, const uint32_t *arms_l,
-                             const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *stream)
+                             const uint32_t *arms_r, int H, int W, int D, int L1, int iters, void *ws, size_t ws_bytes,
+                             void *stream)
 {
-    if (!cv_l || !tmp_l || !cv_r || !tmp_r || !arms_l || !arms_r || H <= 0 || W <= 0 || D <= 0 || iters < 0 ||
-        L1 < 1 || L1 > SDE_CBCA_MAX_L1)
+    if (!cv_l || !tmp_l || !cv_r || !tmp_r || !arms_l || !arms_r || iters < 0 || !cbca_shape_ok(H, W, D, L1) ||
+        (iters > 0 && (!ws || ws_bytes < cbca_ws_bytes(H, W))))
         return SDE_ERR_ARG;
-    // four distinct buffers: each volume's passes run concurrently with the other's
     const float *b[4] = {cv_l, tmp_l, cv_r, tmp_r};
     for (int i = 0; i < 4; i++)
         for (int j = i + 1; j < 4; j++)
             if (b[i] == b[j]) return SDE_ERR_ARG;
-    if (!cbca_shape_ok(H, W, D, L1)) return SDE_ERR_ARG;
-    float *const cvs[2] = {cv_l, cv_r}, *const tmps[2] = {tmp_l, tmp_r};
-    const uint32_t *const refs[2] = {arms_l, arms_r}, *const oths[2] = {arms_r, arms_l};
-    const int sides[2] = {SDE_SIDE_LEFT, SDE_SIDE_RIGHT};
-    return cbca_launch(cvs, tmps, refs, oths, sides, 2, H, W, D, L1, iters, as_stream(stream));
+    int s = cbca_left(cv_l, tmp_l, arms_l, arms_r, H, W, D, L1, iters, ws, as_stream(stream));
+    if (s != SDE_OK) return s;
+    return cbca_right(cv_r, tmp_r, arms_l, arms_r, H, W, D, L1, iters, ws, as_stream(stream));
+}
+
+SDE_EXPORT int sde_cbca_lr(float *cv_l, float *cv_r, float *tmp, const uint32_t *arms_l, const uint32_t *arms_r,
+                           int H, int W, int D, int L1, int iters, void *ws, size_t ws_bytes, void *stream)
+{
+    if (!cv_l || !cv_r || !tmp || !arms_l || !arms_r || iters < 0 || cv_l == cv_r || cv_l == tmp || cv_r == tmp ||
+        !cbca_shape_ok(H, W, D, L1) || (iters > 0 && (!ws || ws_bytes < cbca_ws_bytes(H, W))))
+        return SDE_ERR_ARG;
+    if (iters == 0) return SDE_OK;
+    const int s = cbca_left(cv_l, tmp, arms_l, arms_r, H, W, D, L1, iters, ws, as_stream(stream));
+    if (s != SDE_OK) return s;
+    cbca_rotate(cv_l, cv_r, H, W, D, +1, true, as_stream(stream));
+    return launch_status();
+}
+
+SDE_EXPORT int sde_cbca_reciprocals(double *out, int n, void *stream)
+{
+    if (!out || n <= 0) return SDE_ERR_ARG;
+    cbca_recip_kernel<<<cdiv(n, 256), 256, 0, as_stream(stream)>>>(out, n);
+    return launch_status();
 }

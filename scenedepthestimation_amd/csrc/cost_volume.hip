@@ -700,10 +700,14 @@ __device__ __forceinline__ void c3_unit(cd_u32x4 rs, int gbase, uint32_t lds_uni
     }
 }
 
+// WR: also the right volume.  Without it (the aggregation path: sde_cbca_lr writes the right volume as the
+// aggregated left one's shear) the strips end at the row end and half the stores go.
+template <bool WR>
 __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
                                                        int H, int W, int D, int nchunks, float invalid,
                                                        float *__restrict__ outl, float *__restrict__ outr)
 {
+    constexpr int NST = WR ? 32 : 16;                   // emission stores per strip
     extern __shared__ __attribute__((aligned(16))) char c3_sm[];
     const char *ring = c3_sm;
     const char *own = c3_sm + C3_RING_BYTES;
@@ -723,10 +727,10 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
     const cd_u32x4 rs_r = cd_desc(fr + rowvox * 64, (uint32_t)W * 256u);   // other side's
     // row y of each volume (the host guarantees 4 W D < CD_OOB)
     const __amdgpu_buffer_rsrc_t rl = cd_rsrc(outl + rowvox * D, (uint32_t)W * D * 4u);
-    const __amdgpu_buffer_rsrc_t rr = cd_rsrc(outr + rowvox * D, (uint32_t)W * D * 4u);
+    const __amdgpu_buffer_rsrc_t rr = cd_rsrc(WR ? outr + rowvox * D : outl, (uint32_t)W * D * 4u);
     // strips: the emission after strip k completes R rows [q0-dc-63, q0-dc] (whatever nd), so
-    // the last strip holds x = W-1+dc+63
-    const int nstrips = (W + dc + 62) / C3_NX + 1;
+    // the last strip holds x = W-1+dc+63 (left volume only: the last strip holds x = W-1)
+    const int nstrips = WR ? (W + dc + 62) / C3_NX + 1 : (W + C3_NX - 1) / C3_NX;
 
     // a 64-row block of other-side rows at r (a multiple of 64): parity par, instructions [n0, n1)
     auto ring_unit = [&](int r, int par, int n0, int n1) {
@@ -767,7 +771,7 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
     auto emit_store = [&](int qp, int j) {
         const int rowstep = 16 * D;                         // 4 rows of the volume, bytes
 #pragma unroll
-        for (int n = 8 * j; n < 8 * j + 8 && n < 32; n++) {
+        for (int n = 8 * j; n < 8 * j + 8 && n < NST; n++) {
             if (n < 16) {
                 const int x = qp + wave + 4 * n;
                 const uint32_t so = x < W ? (uint32_t)(((qp + wave) * D + dc) * 4 + n * rowstep) : C3_SKIPOFF;
@@ -799,7 +803,8 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
         // before the second barrier.
         if (!C3_EARLY || k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if (k == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else if (WR) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
         cd_barrier();
         f32x2 own_a[32], own_b[32];
         if (compute) {
@@ -887,7 +892,7 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
     cd_barrier();
     emit_load();
 #pragma unroll
-    for (int j = 0; j < 4; j++) emit_store((nstrips - 1) * C3_NX, j);
+    for (int j = 0; j < NST / 8; j++) emit_store((nstrips - 1) * C3_NX, j);
 }
 
 // Any channel count: one lane per (pixel, d-range), features read from global
@@ -1298,28 +1303,32 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
         if (layout == SDE_LAYOUT_DHW) {
             cv64_kernel<SDE_SIDE_LEFT, OUT_DHW><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid, out_left,
                                                                        nullptr, nullptr, nullptr);
-        } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
-            // one row sweep per (row, 64-disparity chunk) writes both volumes
-            static std::atomic<uint64_t> attr{0};
-            const bool ok = once_per_device(attr, [] {
-                return hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_row_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CVR_SMEM) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr_dma_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)CD_SMEM) == hipSuccess &&
-                       hipFuncSetAttribute(reinterpret_cast<const void *>(cvlr3_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)C3_SMEM) == hipSuccess;
-            });
-            if (!ok) return SDE_ERR_LAUNCH;
+        } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT) ||
+                   (sides == SDE_SIDE_LEFT && CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB)) {
+            // one row sweep per (row, 64-disparity chunk) writes both volumes (the left one alone: the
+            // same sweep without the right volume's stores).  The >64 KB dynamic-LDS opt-in is set for
+            // the kernel that launches, once per device.
             const int nchunks = cdiv(D, CV_DC);
-            if (CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB)
-                cvlr3_kernel<<<dim3((unsigned)(nchunks * H)), 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
-                                                                          out_left, out_right);
-            else if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB)
-                cvlr_dma_kernel<<<dim3((unsigned)(nchunks * H)), 512, CD_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid,
-                                                                             out_left, out_right);
-            else
-                cvlr_row_kernel<<<dim3((unsigned)(nchunks * H)), 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks,
-                                                                             invalid, out_left, out_right);
+            const dim3 grid1((unsigned)(nchunks * H));
+            auto opt_in = [](std::atomic<uint64_t> &done, const void *k, size_t bytes) {
+                return once_per_device(done, [k, bytes] {
+                    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
+                });
+            };
+            static std::atomic<uint64_t> a3l{0}, a3{0}, ad{0}, ar{0};
+            if (sides == SDE_SIDE_LEFT) {
+                if (!opt_in(a3l, reinterpret_cast<const void *>(cvlr3_kernel<false>), C3_SMEM)) return SDE_ERR_LAUNCH;
+                cvlr3_kernel<false><<<grid1, 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, nullptr);
+            } else if (CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB) {
+                if (!opt_in(a3, reinterpret_cast<const void *>(cvlr3_kernel<true>), C3_SMEM)) return SDE_ERR_LAUNCH;
+                cvlr3_kernel<true><<<grid1, 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
+            } else if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB) {
+                if (!opt_in(ad, reinterpret_cast<const void *>(cvlr_dma_kernel), CD_SMEM)) return SDE_ERR_LAUNCH;
+                cvlr_dma_kernel<<<grid1, 512, CD_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
+            } else {
+                if (!opt_in(ar, reinterpret_cast<const void *>(cvlr_row_kernel), CVR_SMEM)) return SDE_ERR_LAUNCH;
+                cvlr_row_kernel<<<grid1, 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
+            }
         } else {
             if (sides & SDE_SIDE_LEFT)
                 cv64_kernel<SDE_SIDE_LEFT, OUT_HWD><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid,

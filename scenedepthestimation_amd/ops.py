@@ -509,31 +509,69 @@ def cbca_arms(img, L1=14, tau=0.02, out=None):
     return out
 
 
-def cbca(cv_hwd, arms_ref, arms_other, side="left", L1=14, iters=2, tmp=None):
+def cbca_workspace_bytes(H, W):
+    """Bytes of the aggregation workspace (column-major arms of both images, sde_cbca_workspace_bytes)."""
+    return int(lib.sde_cbca_workspace_bytes(int(H), int(W)))
+
+
+def _cbca_ws(ws, H, W, like):
+    n = cbca_workspace_bytes(H, W)
+    if ws is None:
+        return _empty((n,), torch.uint8, like), n
+    if not isinstance(ws, torch.Tensor) or not ws.is_cuda or ws.numel() * ws.element_size() < n:
+        raise ValueError(f"cbca workspace must be a GPU tensor of at least {n} bytes")
+    return ws, ws.numel() * ws.element_size()
+
+
+def cbca(cv_hwd, arms_ref, arms_other, side="left", L1=14, iters=2, tmp=None, workspace=None):
     """In-place cross-based aggregation of an [H,W,D] volume (sde_cbca); tmp: same-size scratch."""
     H, W, D = cv_hwd.shape
     if tmp is None:
         tmp = torch.empty_like(cv_hwd)
+    ws, nws = _cbca_ws(workspace, H, W, cv_hwd)
     sd = {"left": SDE_SIDE_LEFT, "right": SDE_SIDE_RIGHT}[side]
     check(lib.sde_cbca(_need(cv_hwd, "cost volume"), _need(tmp, "tmp", shape=(H, W, D)),
                        _need(arms_ref, "arms_ref", dtype=torch.int32, shape=(H, W)),
                        _need(arms_other, "arms_other", dtype=torch.int32, shape=(H, W)), H, W, D, sd, int(L1),
-                       int(iters), _stream()), "sde_cbca")
+                       int(iters), ws.data_ptr(), nws, _stream()), "sde_cbca")
     return cv_hwd
 
 
-def cbca_pair(cv_l, cv_r, arms_l, arms_r, L1=14, iters=2, tmp_l=None, tmp_r=None):
-    """cbca(cv_l, arms_l, arms_r, "left") and cbca(cv_r, arms_r, arms_l, "right") in one launch per pass
+def cbca_pair(cv_l, cv_r, arms_l, arms_r, L1=14, iters=2, tmp_l=None, tmp_r=None, workspace=None):
+    """cbca(cv_l, arms_l, arms_r, "left") and cbca(cv_r, arms_r, arms_l, "right") for any two volumes
     (sde_cbca_pair), in place; tmp_l / tmp_r: same-size scratch, distinct from every volume."""
     H, W, D = cv_l.shape
     tmp_l = torch.empty_like(cv_l) if tmp_l is None else tmp_l
     tmp_r = torch.empty_like(cv_l) if tmp_r is None else tmp_r
+    ws, nws = _cbca_ws(workspace, H, W, cv_l)
     check(lib.sde_cbca_pair(_need(cv_l, "cost volume"), _need(tmp_l, "tmp", shape=(H, W, D)),
                             _need(cv_r, "cost volume", shape=(H, W, D)), _need(tmp_r, "tmp", shape=(H, W, D)),
                             _need(arms_l, "arms_l", dtype=torch.int32, shape=(H, W)),
                             _need(arms_r, "arms_r", dtype=torch.int32, shape=(H, W)), H, W, D, int(L1), int(iters),
-                            _stream()), "sde_cbca_pair")
+                            ws.data_ptr(), nws, _stream()), "sde_cbca_pair")
     return cv_l, cv_r
+
+
+def cbca_lr(cv_l, cv_r, arms_l, arms_r, L1=14, iters=2, tmp=None, workspace=None):
+    """The GPU path's pair (sde_cbca_lr): cv_l aggregated in place, then cv_r's valid voxels set to its
+    shear cv_r[y, x, d] = cv_l[y, x + d, d] (x + d < W; the others untouched).  Equal to cbca_pair when
+    cv_r's valid voxels are cv_l's shear (as cost_volume(..., right=True) writes them)."""
+    H, W, D = cv_l.shape
+    tmp = torch.empty_like(cv_l) if tmp is None else tmp
+    ws, nws = _cbca_ws(workspace, H, W, cv_l)
+    check(lib.sde_cbca_lr(_need(cv_l, "cost volume"), _need(cv_r, "cost volume", shape=(H, W, D)),
+                          _need(tmp, "tmp", shape=(H, W, D)),
+                          _need(arms_l, "arms_l", dtype=torch.int32, shape=(H, W)),
+                          _need(arms_r, "arms_r", dtype=torch.int32, shape=(H, W)), H, W, D, int(L1), int(iters),
+                          ws.data_ptr(), nws, _stream()), "sde_cbca_lr")
+    return cv_l, cv_r
+
+
+def cbca_reciprocals(n, device=None):
+    """The fp64 reciprocals 1/(i+1), i < n, as the aggregation kernels compute them."""
+    out = torch.empty((int(n),), dtype=torch.float64, device=device or torch.device("cuda"))
+    check(lib.sde_cbca_reciprocals(out.data_ptr(), int(n), _stream()), "sde_cbca_reciprocals")
+    return out
 
 
 def lr_check(disp_l, disp_r, lrc_l=None, lrc_r=None):

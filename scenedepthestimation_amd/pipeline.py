@@ -193,7 +193,11 @@ class StereoMatcher:
     def _alloc_sgm(self):
         H, W, D, dev = self.H, self.W, self.D, self.device
         self.sgm_bufs = dict(
-            cv=[torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(2)],
+            # the right volume starts as the GPU path's invalid fill (1.0): with aggregation on, the cost
+            # volume sweep writes the left volume only and sde_cbca_lr the right one's valid voxels, so its
+            # invalid voxels (x + d >= W) keep this fill -- the value the two-volume sweep writes there
+            cv=[torch.empty((H, W, D), dtype=torch.float32, device=dev),
+                torch.full((H, W, D), 1.0, dtype=torch.float32, device=dev)],
             pen=[torch.empty((H, W, 16), dtype=torch.float32, device=dev) for _ in range(2)],
             S=[torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(2)],
             disp=[torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(2)],
@@ -203,6 +207,7 @@ class StereoMatcher:
         )
         if self.cbca_iters > 0:
             self.sgm_bufs["arms"] = [torch.empty((H, W), dtype=torch.int32, device=dev) for _ in range(2)]
+            self.sgm_bufs["cbca_ws"] = torch.empty((ops.cbca_workspace_bytes(H, W),), dtype=torch.uint8, device=dev)
 
     def cbca(self, cv_l, cv_r, img_l, img_r):
         """Cross-based aggregation of the L/R [H,W,D] volumes in place (build-defined).
@@ -215,9 +220,12 @@ class StereoMatcher:
         for k, img in enumerate((img_l, img_r)):
             ops.preprocess_u8(img, P, out=self.img_pad[k], stats=self.stats[k])
             ops.cbca_arms(self.img_pad[k][P:P + H, P:P + W], self.cbca_L1, self.cbca_tau, out=b["arms"][k])
-        # both sides per launch; the SGM S buffers (written later, overwrite mode) are the scratch
-        ops.cbca_pair(cv_l, cv_r, b["arms"][0], b["arms"][1], self.cbca_L1, self.cbca_iters,
-                      tmp_l=b["S"][0], tmp_r=b["S"][1])
+        # the right volume is the left one's shear (valid voxels), so its aggregation is the shear of the
+        # left one's (definition v2): one volume aggregated, then one shear pass writes cv_r's valid voxels
+        # (their input is not read; its invalid voxels are kept).  The SGM S buffer (written later,
+        # overwrite mode) is the scratch.
+        ops.cbca_lr(cv_l, cv_r, b["arms"][0], b["arms"][1], self.cbca_L1, self.cbca_iters, tmp=b["S"][0],
+                    workspace=b["cbca_ws"])
         return cv_l, cv_r
 
     def sgm_path(self, fl=None, fr=None, img_l=None, img_r=None, timings=None, post=True):
@@ -242,8 +250,10 @@ class StereoMatcher:
             return t0
 
         t = time.time() if timings is not None else 0.0
-        ops.cost_volume(fl, fr, self.D, layout="HWD", right=True, invalid=1.0,
-                        out_left=b["cv"][0], out_right=b["cv"][1])
+        # process_functional.py:120-131.  With aggregation the right volume comes from sde_cbca_lr (the
+        # aggregated left volume's shear), so the sweep writes the left one only.
+        ops.cost_volume(fl, fr, self.D, layout="HWD", right=self.cbca_iters <= 0, invalid=1.0,
+                        out_left=b["cv"][0], out_right=b["cv"][1] if self.cbca_iters <= 0 else None)
         t = mark("cost_volume", t)
         if self.cbca_iters > 0:
             self.cbca(b["cv"][0], b["cv"][1], img_l, img_r)

@@ -27,7 +27,18 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_status_strings():
-    assert _lib.lib.sde_abi_version() == 2
+    assert _lib.lib.sde_abi_version() == 3 == _lib.SDE_ABI_VERSION
+    # the header's version is the binding's
+    import re
+    with open(_lib.os.path.join(_lib.INCLUDE, "sde.h")) as fh:
+        assert int(re.search(r"#define SDE_ABI_VERSION (\d+)", fh.read()).group(1)) == _lib.SDE_ABI_VERSION
+
+
+def test_cbca_segment_constant_matches_oracle():
+    import re
+    from oracle import oracle
+    with open(_lib.os.path.join(_lib.INCLUDE, "sde.h")) as fh:
+        assert int(re.search(r"#define SDE_CBCA_SEG (\d+)", fh.read()).group(1)) == oracle.cbca_seg()
     assert _lib.lib.sde_status_string(0) == b"ok"
     assert _lib.lib.sde_status_string(-1) == b"invalid argument"
     assert _lib.lib.sde_status_string(-3) == b"workspace too small"
@@ -127,12 +138,25 @@ def test_argument_validation_without_gpu():
     # [mean, std, -, -] + one float per 8192-pixel piece, rounded to 256 B
     assert lib.sde_preprocess_scratch_bytes(1024, 1024) == 768 and lib.sde_preprocess_scratch_bytes(3, 5) == 256
     assert lib.sde_tower_packed_floats(0, 64) == -1
-    assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 4, 8, 14, 1, N) == ERR                          # aliased buffers
-    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 4, 8, 33, 1, N) == ERR                          # L1 > 32
-    # 32-bit scan offsets: (3R + 18) rows of 4*W*D bytes must stay below 2^31 (R = 15 for L1 <= 16)
-    assert lib.sde_cbca(1, 2, 3, 4, 2, 40000, 256, 1, 14, 0, N) == ERR                            # 63 * 41 MB
-    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 33300, 256, 14, 0, N) == ERR                    # just past
-    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 19000, 256, 20, 0, N) == ERR                    # R = 31: 111 rows
+    W8 = lib.sde_cbca_workspace_bytes(4, 8)
+    assert W8 == 8 * 8 * 4 and lib.sde_cbca_workspace_bytes(5, 7) == 8 * 7 * 8 and lib.sde_cbca_workspace_bytes(0, 7) == 0
+    assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 8, 8, 14, 1, 7, W8, N) == ERR                   # aliased buffers
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 8, 8, 33, 1, 7, W8, N) == ERR                   # L1 > 32
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 8, 8, 14, 1, 7, W8 - 1, N) == ERR               # workspace
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 8, 8, 14, 1, N, W8, N) == ERR                   # no workspace
+    assert lib.sde_cbca(1, 2, 3, 4, 4, 8, 513, 1, 14, 1, 7, W8, N) == ERR                         # D > 512
+    assert lib.sde_cbca(1, 1, 3, 4, 4, 8, 8, 1, 14, 1, 7, W8, N) == ERR                           # cv == tmp
+    assert lib.sde_cbca(1, 2, 3, 4, 4, 8, 8, 3, 14, 1, 7, W8, N) == ERR                           # side
+    assert lib.sde_cbca_lr(1, 2, 2, 4, 5, 4, 8, 8, 14, 1, 7, W8, N) == ERR                        # cv_r == tmp
+    assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 4, 8, 8, 14, 1, 7, W8 - 4, N) == ERR                    # workspace
+    assert lib.sde_cbca_reciprocals(N, 4, N) == ERR
+    # 32-bit offsets: a vertical-pass block window of (5R + 5) rows of 4*W*D bytes stays below 2^31
+    # (R = 13 for L1 <= 14: 70 rows; R = 31 for L1 > 16: 160 rows).  iters = 0 checks the shape only.
+    assert lib.sde_cbca(1, 2, 3, 4, 2, 40000, 256, 1, 14, 0, N, 0, N) == ERR                      # 70 * 41 MB
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 29960, 256, 14, 0, N, 0, N) == ERR              # just past
+    assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 29959, 256, 14, 0, N, 0, N) == 0                # just inside
+    assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 2, 13108, 256, 20, 0, N, 0, N) == ERR                   # R = 31
+    assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 2, 13107, 256, 20, 0, N, 0, N) == 0
     assert lib.sde_lrc_fill(1, 2, 4, 65535, 3, N) == ERR                                          # 16-bit columns
     assert lib.sde_lrc_fill(1, 2, 65535, 4, 3, N) == ERR                                          # 16-bit rows
 

@@ -162,8 +162,8 @@ def _sgm_path_vs_oracle(oracle, H, W, D, seed, cbca_iters=2, L1=14, tau=0.02):
     if cbca_iters:
         _progress("oracle CBCA")
         al, ar = oracle.cbca_arms(zl, L1, tau), oracle.cbca_arms(zr, L1, tau)
-        cl = oracle.cbca(cl, al, ar, "left", cbca_iters)
-        cr = oracle.cbca(cr, ar, al, "right", cbca_iters)
+        cl = oracle.cbca(cl, al, ar, "left", cbca_iters, L1=L1)
+        cr = oracle.cbca(cr, ar, al, "right", cbca_iters, L1=L1)
     def stage_report(k, c, img):
         """on a mismatch: which stage of side k differs (aggregated volume, S after 7 directions)"""
         bad = np.argwhere(gcv[k].view(np.int32) != c.view(np.int32))

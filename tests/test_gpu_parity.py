@@ -125,6 +125,9 @@ def test_hwd_volumes_vs_oracle(gpu, oracle):
         R1 = torch.full((H, W, D), float("nan"), device="cuda")     # right side alone (its own kernel)
         ops.cost_volume(dev(fl), dev(fr), D, layout="HWD", right=True, left=False, invalid=1.0, out_right=R1)
         assert host(R1).tobytes() == oR.tobytes()
+        L1 = torch.full((H, W, D), float("nan"), device="cuda")     # left side alone (the sweep, no R stores)
+        ops.cost_volume(dev(fl), dev(fr), D, layout="HWD", invalid=1.0, out_left=L1)
+        assert host(L1).tobytes() == oL.tobytes()
 
 
 def test_hwd_volumes_nonfinite_features(gpu, oracle):
@@ -338,32 +341,76 @@ def test_sgm_8path_bit_exact(gpu, oracle, H, W, D):
 
 
 @pytest.mark.parametrize("H,W,D,L1,iters", [(23, 61, 40, 14, 2), (40, 33, 130, 16, 1), (70, 12, 7, 32, 2),
-                                             (3, 2, 16, 14, 1), (16, 96, 192, 14, 3)])
+                                             (3, 2, 16, 14, 1), (16, 96, 192, 14, 3), (300, 270, 70, 14, 1)])
 def test_cbca_pair_bit_exact(gpu, oracle, H, W, D, L1, iters):
-    """Both volumes of a pair in one launch per pass == the oracle's per-side aggregation."""
+    """Any two volumes (the right one through the rotation into left coordinates) == the oracle's
+    per-side aggregation; lines longer than one segment (SDE_CBCA_SEG = 256) in the last case."""
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(7 * H + W + D)
     il, ir = _cbca_images(rng, H, W), _cbca_images(rng, H, W)
     al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
     cl = rng.standard_normal((H, W, D)).astype(np.float32)
     cr = rng.standard_normal((H, W, D)).astype(np.float32)
-    want_l, want_r = oracle.cbca(cl, al, ar, "left", iters), oracle.cbca(cr, ar, al, "right", iters)
+    want_l = oracle.cbca(cl, al, ar, "left", iters, L1=L1)
+    want_r = oracle.cbca(cr, ar, al, "right", iters, L1=L1)
     gl, gr = dev(cl), dev(cr)
     ops.cbca_pair(gl, gr, dev(al.view(np.int32)), dev(ar.view(np.int32)), L1, iters)
     assert host(gl).tobytes() == want_l.tobytes()
     assert host(gr).tobytes() == want_r.tobytes()
 
 
+def _sheared_pair(rng, H, W, D, scale=1.0, offset=0.0):
+    """A left volume (invalid voxels x < d at 1.0, as the GPU path fills them) and its right shear."""
+    cl = (rng.standard_normal((H, W, D)) * scale + offset).astype(np.float32)
+    cr = np.ones_like(cl)
+    for d in range(D):
+        cl[:, :min(d, W), d] = 1.0
+        if d < W:
+            cr[:, :W - d, d] = cl[:, d:, d]
+    return cl, cr
+
+
+@pytest.mark.parametrize("H,W,D,L1,iters", [(23, 61, 40, 14, 2), (16, 96, 192, 14, 2), (40, 33, 130, 16, 1),
+                                             (70, 12, 7, 32, 2), (270, 300, 66, 14, 2), (3, 2, 16, 14, 1)])
+def test_cbca_lr_bit_exact(gpu, oracle, H, W, D, L1, iters):
+    """The GPU path's pair: one volume aggregated + the shear == the oracle's sdeo_cbca_lr, and (the
+    right volume being the left one's shear) == aggregating both volumes (cbca_pair)."""
+    from scenedepthestimation_amd import ops
+    rng = np.random.default_rng(11 * H + W + D)
+    il, ir = _cbca_images(rng, H, W), _cbca_images(rng, H, W)
+    al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
+    cl, cr = _sheared_pair(rng, H, W, D, 2.0, 3.0)
+    want_l, want_r = oracle.cbca_lr(cl, cr, al, ar, iters, L1=L1)
+    gl, gr = dev(cl), dev(cr)
+    ops.cbca_lr(gl, gr, dev(al.view(np.int32)), dev(ar.view(np.int32)), L1, iters)
+    assert host(gl).tobytes() == want_l.tobytes()
+    assert host(gr).tobytes() == want_r.tobytes()
+    pl, pr = dev(cl), dev(cr)
+    ops.cbca_pair(pl, pr, dev(al.view(np.int32)), dev(ar.view(np.int32)), L1, iters)
+    assert torch.equal(pl, gl) and torch.equal(pr, gr)
+
+
+def test_cbca_reciprocals_correctly_rounded(gpu):
+    """The mean's 1/count (v_rcp_f64 + two Newton steps) is the IEEE quotient for every count the
+    definition can produce: (2 * 31 + 1)^2 at L1 = 32."""
+    from scenedepthestimation_amd import ops
+    n = 63 * 63
+    got = ops.cbca_reciprocals(n).cpu().numpy()
+    want = 1.0 / np.arange(1, n + 1, dtype=np.float64)
+    assert got.tobytes() == want.tobytes()
+
+
 def test_cbca_pair_bench_width_bit_exact(gpu, oracle):
     """A band of rows at the benchmark's width and D (1024 x 192): every x - d / x + d edge regime."""
     test_cbca_pair_bit_exact(gpu, oracle, 24, 1024, 192, 14, 2)
+    test_cbca_lr_bit_exact(gpu, oracle, 24, 1024, 192, 14, 2)
 
 
 def test_cbca_pair_config3_identity(gpu):
-    """Middlebury-2014 scale (2000 x 3000 x 256: 6 GB per volume, the V pass's offsets beyond 32 bits):
+    """Middlebury-2014 scale (2000 x 3000 x 256: 6 GB per volume, a column's offsets beyond 32 bits):
     with zero arms every support is the pixel itself, and for small-integer costs the fp64 prefix
     differences are exact, so both volumes must come back unchanged bit for bit -- any misaddressed
-    row, column or disparity changes a value."""
+    row, column or disparity changes a value (the right one also through both rotations)."""
     from scenedepthestimation_amd import ops
     H, W, D = 2000, 3000, 256
     y = torch.arange(H, device="cuda").view(H, 1, 1)
@@ -376,6 +423,15 @@ def test_cbca_pair_config3_identity(gpu):
     ops.cbca_pair(gl, gr, arms, arms, 14, 1)
     torch.cuda.synchronize()
     assert torch.equal(gl, cl) and torch.equal(gr, cr)
+    del gl, gr
+    # the shear: every valid right voxel becomes the left voxel at x + d, the invalid ones stay
+    gl, gr = cl.clone(), cr.clone()
+    ops.cbca_lr(gl, gr, arms, arms, 14, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(gl, cl)
+    xs = x + d
+    want = torch.where(xs < W, ((7 * y + 3 * xs + d) % 13).float(), cr)
+    assert torch.equal(gr, want)
 
 
 @pytest.mark.parametrize("H,W,D", [(33, 70, 97), (19, 41, 192), (5, 130, 64), (70, 9, 300), (2, 50, 64)])
@@ -430,7 +486,8 @@ def test_cbca_arms_bit_exact(gpu, oracle, L1, tau):
 @pytest.mark.parametrize("H,W,D,L1,iters,side", [(23, 61, 40, 14, 2, "left"), (40, 33, 100, 16, 1, "right"),
                                                  (9, 130, 64, 20, 1, "left"), (70, 12, 7, 32, 2, "right"),
                                                  (5, 5, 3, 14, 0, "left"), (16, 96, 192, 14, 2, "left"),
-                                                 (12, 300, 256, 14, 1, "left")])
+                                                 (12, 300, 256, 14, 1, "left"), (300, 40, 70, 14, 2, "right"),
+                                                 (280, 23, 30, 14, 1, "left")])
 def test_cbca_bit_exact(gpu, oracle, H, W, D, L1, iters, side):
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(H * W + D)
@@ -438,7 +495,7 @@ def test_cbca_bit_exact(gpu, oracle, H, W, D, L1, iters, side):
     al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
     ref, oth = (al, ar) if side == "left" else (ar, al)
     cv = rng.standard_normal((H, W, D)).astype(np.float32)
-    want = oracle.cbca(cv, ref, oth, side, iters)
+    want = oracle.cbca(cv, ref, oth, side, iters, L1=L1)
     got = dev(cv)
     ops.cbca(got, dev(ref.view(np.int32)), dev(oth.view(np.int32)), side, L1, iters)
     assert host(got).tobytes() == want.tobytes()
@@ -489,7 +546,7 @@ def test_matcher_cbca_sgm_end_to_end(gpu, oracle):
     al, ar = oracle.cbca_arms(zl, 14, 0.5), oracle.cbca_arms(zr, 14, 0.5)
     assert ((al & 255) > 0).mean() > 0.2              # the arms are not trivial at this tau
     cl, cr = oracle.cost_volume_hwd(fl, fr, D, invalid=1.0, right=True)
-    cl, cr = oracle.cbca(cl, al, ar, "left", 2), oracle.cbca(cr, ar, al, "right", 2)
+    cl, cr = oracle.cbca(cl, al, ar, "left", 2, L1=14), oracle.cbca(cr, ar, al, "right", 2, L1=14)
     Sl = oracle.sgm_8path(cl, oracle.sgm_penalties(left))
     Sr = oracle.sgm_8path(cr, oracle.sgm_penalties(right))
     assert np.array_equal(host(dl), oracle.wta_sgm(Sl))

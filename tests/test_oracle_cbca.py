@@ -28,38 +28,58 @@ def arms_literal(img, L1, tau):
     return out
 
 
+SEG = 256   # SDE_CBCA_SEG
+
+
 def support(ref, oth, y, x, d, side):
+    """Support arms of voxel (y, x, d) in its own coordinates (None if invalid)."""
     W = ref.shape[1]
     o = x - d if side == "left" else x + d
     if not 0 <= o < W:
-        return [0, 0, 0, 0]
+        return None
     return [min((int(ref[y, x]) >> (8 * k)) & 255, (int(oth[y, o]) >> (8 * k)) & 255) for k in range(4)]
 
 
-def cbca_literal(cv, ref, oth, side, iters):
+def cbca_literal(cv, ref, oth, side, iters, L1):
+    """Definition v2 stated voxel by voxel in the volume's OWN coordinates: a right-referenced
+    voxel x' sits at left coordinate q = x' + d, which fixes its segment and chain base."""
     H, W, D = cv.shape
+    M = L1 - 1
+    lq = (lambda x, d: x) if side == "left" else (lambda x, d: x + d)     # left coordinate
+    xq = (lambda q, d: q) if side == "left" else (lambda q, d: q - d)     # back to own coordinate
     cur = cv.copy()
     for _ in range(iters):
-        T = np.zeros_like(cur)
+        T = cur.copy()                                       # invalid voxels pass through
         for y in range(H):
             for d in range(D):
-                P = [0.0]
-                for x in range(W):
-                    P.append(P[-1] + float(cur[y, x, d]))          # Python float = IEEE fp64
                 for x in range(W):
                     a = support(ref, oth, y, x, d, side)
-                    T[y, x, d] = np.float32(P[x + a[1] + 1] - P[x - a[0]])
-        nxt = np.zeros_like(cur)
+                    if a is None:
+                        continue
+                    q = lq(x, d)
+                    k = q // SEG
+                    b = max(k * SEG - M, d)                  # chain base (left coordinates)
+                    P = {b - 1: 0.0}
+                    for i in range(b, q + a[1] + 1):
+                        P[i] = P[i - 1] + float(cur[y, xq(i, d), d])   # Python float = IEEE fp64
+                    T[y, x, d] = np.float32(P[q + a[1]] - P[q - a[0] - 1])
+        nxt = T.copy()
         for x in range(W):
             for d in range(D):
-                Q, N = [0.0], [0]
-                for y in range(H):
-                    b = support(ref, oth, y, x, d, side)
-                    Q.append(Q[-1] + float(T[y, x, d]))
-                    N.append(N[-1] + b[0] + b[1] + 1)
                 for y in range(H):
                     a = support(ref, oth, y, x, d, side)
-                    nxt[y, x, d] = np.float32((Q[y + a[3] + 1] - Q[y - a[2]]) / float(N[y + a[3] + 1] - N[y - a[2]]))
+                    if a is None:
+                        nxt[y, x, d] = cur[y, x, d]
+                        continue
+                    k = y // SEG
+                    b = max(k * SEG - M, 0)
+                    Q, N = {b - 1: 0.0}, {b - 1: 0}
+                    for i in range(b, y + a[3] + 1):
+                        s = support(ref, oth, i, x, d, side)
+                        Q[i] = Q[i - 1] + float(T[i, x, d])
+                        N[i] = N[i - 1] + s[0] + s[1] + 1
+                    cnt = N[y + a[3]] - N[y - a[2] - 1]
+                    nxt[y, x, d] = np.float32((Q[y + a[3]] - Q[y - a[2] - 1]) * (1.0 / float(cnt)))
         cur = nxt
     return cur
 
@@ -87,8 +107,50 @@ def test_cbca_matches_literal(side, iters):
     al, ar = oracle.cbca_arms(il, 5, 0.03), oracle.cbca_arms(ir, 5, 0.03)
     ref, oth = (al, ar) if side == "left" else (ar, al)
     cv = rng.standard_normal((H, W, D)).astype(np.float32)
-    got = oracle.cbca(cv, ref, oth, side, iters)
-    assert got.tobytes() == cbca_literal(cv, ref, oth, side, iters).tobytes()
+    got = oracle.cbca(cv, ref, oth, side, iters, L1=5)
+    assert got.tobytes() == cbca_literal(cv, ref, oth, side, iters, 5).tobytes()
+
+
+@pytest.mark.parametrize("side,H,W", [("left", 5, 300), ("right", 5, 300), ("left", 290, 6), ("right", 290, 6)])
+def test_cbca_segments_match_literal(side, H, W):
+    """Lines longer than one segment (SDE_CBCA_SEG = 256): chains restart at kS - M."""
+    assert oracle.cbca_seg() == SEG
+    rng = np.random.default_rng(11)
+    D = 3
+    il, ir = _images(rng, H, W), _images(rng, H, W)
+    al, ar = oracle.cbca_arms(il, 6, 0.06), oracle.cbca_arms(ir, 6, 0.06)
+    ref, oth = (al, ar) if side == "left" else (ar, al)
+    cv = (rng.standard_normal((H, W, D)) * 3 + 20).astype(np.float32)   # far from 0: rounding matters
+    got = oracle.cbca(cv, ref, oth, side, 1, L1=6)
+    assert got.tobytes() == cbca_literal(cv, ref, oth, side, 1, 6).tobytes()
+
+
+def _shear(cl):
+    """Right-referenced volume of a left one: R(y, x', d) = L(y, x'+d, d), invalid voxels 1.0."""
+    H, W, D = cl.shape
+    cr = np.ones_like(cl)
+    for d in range(D):
+        cr[:, :W - d, d] = cl[:, d:, d]
+    return cr
+
+
+@pytest.mark.parametrize("L1,iters", [(14, 2), (5, 1)])
+def test_cbca_right_is_shear_of_left(L1, iters):
+    """CBCA(R) = shear(CBCA(L)) exactly when R = shear(L): the one support of both volumes, and the
+    pair entry point (left aggregated, right sheared) equals aggregating both."""
+    rng = np.random.default_rng(5)
+    H, W, D = 9, 270, 12
+    il, ir = _images(rng, H, W), _images(rng, H, W)
+    al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
+    cl = (rng.standard_normal((H, W, D)) + 5).astype(np.float32)
+    for d in range(D):
+        cl[:, :d, d] = 1.0                                  # the GPU path's invalid fill
+    cr = _shear(cl)
+    left = oracle.cbca(cl, al, ar, "left", iters, L1=L1)
+    right = oracle.cbca(cr, ar, al, "right", iters, L1=L1)
+    assert right.tobytes() == _shear(left).tobytes()
+    lr_l, lr_r = oracle.cbca_lr(cl, cr, al, ar, iters, L1=L1)
+    assert lr_l.tobytes() == left.tobytes() and lr_r.tobytes() == right.tobytes()
 
 
 def test_cbca_properties():
@@ -99,8 +161,8 @@ def test_cbca_properties():
     zero = oracle.cbca_arms(flat, 14, 0.0)                 # tau = 0: no arms -> identity (up to the prefix
     np.testing.assert_allclose(oracle.cbca(cv, zero, zero, "left", 3), cv, rtol=1e-7, atol=1e-12)  # rounding)
     assert oracle.cbca(cv, zero, zero, "left", 0).tobytes() == cv.tobytes()
-    full = oracle.cbca_arms(flat, 64, 1.0)                 # flat image, long arms: support = whole image
-    out = oracle.cbca(cv, full, full, "left", 1)
+    full = oracle.cbca_arms(flat, 32, 1.0)                 # flat image, long arms: support = whole image
+    out = oracle.cbca(cv, full, full, "left", 1, L1=32)
     for d in range(D):
         # left-referenced: voxels with x >= d average over the region x' >= d; x < d stays as is
         np.testing.assert_allclose(out[:, d:, d], cv[:, d:, d].mean(), rtol=2e-5, atol=2e-6)
