@@ -439,7 +439,9 @@ def main():
     for _ in range(min(args.steps, 5)):
         step(timed="stages")
     torch.cuda.synchronize()
-    tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    # max over ranks (gloo reduces host tensors: SDE_DIST_BACKEND=gloo runs ranks on a shared GPU)
+    tt = torch.tensor([elapsed], dtype=torch.float64,
+                      device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())

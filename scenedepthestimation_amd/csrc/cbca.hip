@@ -32,6 +32,8 @@
 //    lane per four rows.
 #include "sde_common.h"
 
+#include <algorithm>
+
 namespace sde {
 
 __global__ __launch_bounds__(256) void cbca_arms_kernel(const float *__restrict__ img, int64_t pitch, int H, int W,
@@ -131,14 +133,9 @@ struct CbcaArgs {
     int H, W, D, M, Hp;
     int nseg, ndc;
     int64_t nitems;
-    int per;                       // items per wave (contiguous range)
-    int64_t chunk_first[9];        // vertical pass: first item of chunk c (valid columns only)
+    int64_t nper;                  // items per segment (vertical pass: valid (column, chunk) pairs only)
 };
 
-// ---------------------------------------------------------------------------------------------
-// Horizontal pass: item = (row y, chunk c, segment k), k fastest, so a wave's consecutive items
-// are consecutive segments of one row.
-// ---------------------------------------------------------------------------------------------
 // Opaque to the optimiser: keeps a per-step offset an incremented register instead of 2R+2
 // block-invariant constants hoisted out of the loop (SGPR pressure, spills, drained prefetch).
 __device__ __forceinline__ uint32_t opq_s(uint32_t v)
@@ -152,6 +149,10 @@ __device__ __forceinline__ uint32_t opq_v(uint32_t v)
     return v;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Horizontal pass: item = (segment k, row y, chunk c), c fastest; wave w takes items w, w + G, ...,
+// so the waves in flight walk the same segment of consecutive rows, a pixel's chunks side by side.
+// ---------------------------------------------------------------------------------------------
 template <int R>
 __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int k, double *__restrict__ sP)
 {
@@ -180,21 +181,24 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
         av = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(tb + lane), 0, 0);
         bv = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(tb + lane - d0), 0, 0);
     };
+    // the arms first: a loop-carried register loaded after the cost prefetch would make the entry
+    // path's wait for it (merged into every block start) drain the whole prefetch
+    uint32_t A0, B0, A1, B1;
+    arms_blk(fs - R, A0, B0);
+    arms_blk(fs + RS - R, A1, B1);
+    // right-image arm of the trailing position, lane i = pixel t - d0 - i: the state before step fs
+    uint32_t X = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(fs - R - 1 - d0 - lane), 0, 0);
 #pragma unroll
     for (int j = 0; j < PF; j++)
         cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)(D4 * (uint32_t)min(fs + j, W - 1)),
                                                                                CBCA_NT & 1 ? 2 : 0));
-    uint32_t Ab, Bb, An, Bn;
-    arms_blk(fs - R, Ab, Bb);
-    // right-image arm of the trailing position, lane i = pixel t - d0 - i: the state before step fs
-    uint32_t X = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(fs - R - 1 - d0 - lane), 0, 0);
     double P = 0.0;
     sP[(RS - 1) * 64 + lane] = 0.0;               // P(fs - 1) = 0: read before position fs + RS - 1 lands
     // per-lane store offset of output t (4d + 4tD), advanced every step
     uint32_t vst = 4u * (uint32_t)d + D4 * (uint32_t)(fs - R);
 
     // step j of a block at front f; CLAMP: prefetch positions may pass the row end (tail blocks)
-    auto step = [&](int j, int f, uint32_t &sld, bool clamp) {
+    auto step = [&](int j, int f, uint32_t Ab, uint32_t Bb, uint32_t &sld, bool clamp) {
         const int slot = j % PF;
         // front: the chain of this lane starts at max(t0 - M, d) >= fs
         const float cv = cr[slot];
@@ -216,24 +220,44 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
                                               CBCA_NT & 2 ? 2 : 0);
         vst = opq_v(vst + D4);
     };
+    // Blocks of RS steps.  The block arms alternate between two register pairs, each reloaded in
+    // place at the end of the block it served with the arms of the block after next (issued a whole
+    // block before use; no loop-carried copy of a register with a load in flight, which would wait
+    // for it -- and, vmcnt retiring in order, drain the cost prefetch).  The first two blocks are
+    // peeled and the loop runs two blocks per iteration, so the loop header merges steady-state
+    // waits only.  Main blocks have every front and prefetch position inside the row; the tail
+    // blocks clamp.
     int fb = fs;
-    // main blocks: every front and prefetch position inside the row
-    for (; fb + RS - 1 <= fe && fb + RS - 1 + PF <= W - 1; fb += RS) {
-        arms_blk(fb + RS - R, An, Bn);
+    auto block = [&](uint32_t &Ap, uint32_t &Bp, bool clamp) {
         uint32_t sld = D4 * (uint32_t)(fb + PF);
 #pragma unroll
-        for (int j = 0; j < RS; j++) step(j, fb + j, sld, false);
-        Ab = An;
-        Bb = Bn;
-    }
-    for (; fb <= fe; fb += RS) {
-        arms_blk(fb + RS - R, An, Bn);
-        uint32_t sld = 0;
-#pragma unroll
         for (int j = 0; j < RS; j++)
-            if (fb + j <= fe) step(j, fb + j, sld, true);
-        Ab = An;
-        Bb = Bn;
+            if (!clamp || fb + j <= fe) step(j, fb + j, Ap, Bp, sld, clamp);
+        arms_blk(fb + 2 * RS - R, Ap, Bp);
+        fb += RS;
+    };
+    auto full = [&]() { return fb + RS - 1 <= fe && fb + RS - 1 + PF <= W - 1; };
+    bool odd = false;
+    if (full()) {
+        block(A0, B0, false);
+        odd = true;
+        if (full()) {
+            block(A1, B1, false);
+            odd = false;
+            while (full()) {
+                block(A0, B0, false);
+                if (!full()) {
+                    odd = true;
+                    break;
+                }
+                block(A1, B1, false);
+            }
+        }
+    }
+    while (fb <= fe) {
+        if (odd) block(A1, B1, true);
+        else block(A0, B0, true);
+        odd = !odd;
     }
 }
 
@@ -241,17 +265,17 @@ template <int R>
 __global__ __launch_bounds__(64, 3) void cbca_h_kernel(const CbcaArgs A)
 {
     __shared__ double sP[(2 * R + 2) * 64];
-    const int64_t i0 = (int64_t)blockIdx.x * A.per, i1 = min(i0 + A.per, A.nitems);
-    for (int64_t it = i0; it < i1; it++) {
-        const int k = (int)(it % A.nseg);
-        const int64_t r = it / A.nseg;
+    for (int64_t it = blockIdx.x; it < A.nitems; it += gridDim.x) {
+        const int k = (int)(it / A.nper);
+        const int64_t r = it - (int64_t)k * A.nper;
         cbca_h_item<R>(A, (int)(r / A.ndc), (int)(r % A.ndc), k, sP);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Vertical pass: item = (chunk c, column x >= 64c, segment k), k fastest; only columns with at
-// least one valid lane (x >= d0) are items.
+// Vertical pass: item = (segment k, column x, chunk c <= x / 64), c fastest (only chunks with a
+// valid lane are items); wave w takes items w, w + G, ...: the waves in flight walk the same rows
+// of consecutive columns, so each row step reads whole pixels side by side.
 // ---------------------------------------------------------------------------------------------
 template <int R>
 __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, double *__restrict__ sP,
@@ -279,12 +303,18 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     float cr[PF];
     u32x4 Bq[NQ];                // right-image arms of rows fb + 4m .. +3 (per lane); Bq[m] is
                                  // reloaded with the next block's rows once its last row is used
-    uint32_t Ab, An;             // left-image arm of row fb + lane (lanes < RS)
+    uint32_t A0, A1;             // left-image arm of row fb + lane (lanes < RS), pairs by block parity
     uint32_t sup[U];             // (vu | vd << 16) of the last U front positions
     auto arm_q = [&](int row) {  // rows row .. row + 3 of the right image at x - d
         const uint32_t off = bcol == CB_OOB ? CB_OOB : bcol + 4u * (uint32_t)row;
         return __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
     };
+    // the arms first: loop-carried registers loaded after the cost prefetch would make the entry
+    // path's waits for them (merged into every block start) drain the whole prefetch
+    A0 = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + lane), 0, 0);
+    A1 = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + RS + lane), 0, 0);
+#pragma unroll
+    for (int m = 0; m < NQ; m++) Bq[m] = arm_q(fs + 4 * m);
     {
         const __amdgpu_buffer_rsrc_t rc0 = cb_rsrc(A.src + ((size_t)fs * W + x) * D, win);
 #pragma unroll
@@ -292,9 +322,6 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
             cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                   rc0, dl4, (int)(rowv * (uint32_t)(min(fs + j, H - 1) - fs)), CBCA_NT & 1 ? 2 : 0));
     }
-    Ab = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + lane), 0, 0);
-#pragma unroll
-    for (int m = 0; m < NQ; m++) Bq[m] = arm_q(fs + 4 * m);
 #pragma unroll
     for (int j = 0; j < U; j++) sup[j] = 0u;
     double P = 0.0;
@@ -303,8 +330,8 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     sN[(RS - 1) * 64 + lane] = 0;
 
     // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R
-    auto step = [&](int j, int f, int fbase, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rd, uint32_t &sld,
-                    uint32_t &sst, bool clamp) {
+    auto step = [&](int j, int f, int fbase, uint32_t Ab, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rd,
+                    uint32_t &sld, uint32_t &sst, bool clamp) {
         const int slot = j % PF;
         // front f: chain (rows >= fc), count contribution and vertical support
         const uint32_t a = ruint(Ab, j);
@@ -339,41 +366,70 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         sst = opq_s(sst + rowv);
     };
     int fb = fs;
-    for (; fb + RS - 1 <= fe && fb + RS - 1 + PF <= H - 1; fb += RS) {
-        An = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + RS + lane), 0, 0);
-        // loads for positions fb + PF .. go against a descriptor rebased on row fb
-        const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fb * W + x) * D, win);
+    // blocks as in the horizontal pass: two alternating left-arm registers reloaded in place, the
+    // first two blocks peeled, two blocks per loop iteration, clamped tail blocks
+    auto block = [&](uint32_t &Ap, bool clamp) {
+        // loads for positions fb + PF .. go against a descriptor rebased on row fbase (a tail block
+        // may start past the last row), stores against one rebased on row fb - R
+        const int fbase = clamp ? min(fb, H - 1) : fb;
+        const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fbase * W + x) * D, win);
         const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R) * W + x) * D, win);
         uint32_t sld = rowv * (uint32_t)PF, sst = 0;
 #pragma unroll
-        for (int j = 0; j < RS; j++) step(j, fb + j, fb, rc, rd, sld, sst, false);
-        Ab = An;
-    }
-    for (; fb <= fe; fb += RS) {
-        An = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + RS + lane), 0, 0);
-        const int fbase = min(fb, H - 1);       // a tail block may start past the last row
-        const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fbase * W + x) * D, win);
-        const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R) * W + x) * D, win);
-        uint32_t sld = 0, sst = 0;
-#pragma unroll
         for (int j = 0; j < RS; j++)
-            if (fb + j <= fe) step(j, fb + j, fbase, rc, rd, sld, sst, true);
-        Ab = An;
+            if (!clamp || fb + j <= fe) step(j, fb + j, fbase, Ap, rc, rd, sld, sst, clamp);
+        Ap = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + 2 * RS + lane), 0, 0);
+        fb += RS;
+    };
+    auto full = [&]() { return fb + RS - 1 <= fe && fb + RS - 1 + PF <= H - 1; };
+    bool odd = false;
+    if (full()) {
+        block(A0, false);
+        odd = true;
+        if (full()) {
+            block(A1, false);
+            odd = false;
+            while (full()) {
+                block(A0, false);
+                if (!full()) {
+                    odd = true;
+                    break;
+                }
+                block(A1, false);
+            }
+        }
+    }
+    while (fb <= fe) {
+        if (odd) block(A1, true);
+        else block(A0, true);
+        odd = !odd;
     }
 }
 
 template <int R>
-__global__ __launch_bounds__(64, 3) void cbca_v_kernel(const CbcaArgs A)
+__global__ __launch_bounds__(64, 2) void cbca_v_kernel(const CbcaArgs A)
 {
     __shared__ double sP[(2 * R + 2) * 64];
     __shared__ uint16_t sN[(2 * R + 2) * 64];
-    const int64_t i0 = (int64_t)blockIdx.x * A.per, i1 = min(i0 + A.per, A.nitems);
-    for (int64_t it = i0; it < i1; it++) {
-        int c = 0;
-        while (c + 1 < A.ndc && it >= A.chunk_first[c + 1]) c++;
-        const int64_t r = it - A.chunk_first[c];
-        const int k = (int)(r % A.nseg);
-        cbca_v_item<R>(A, 64 * c + (int)(r / A.nseg), c, k, sP, sN);
+    for (int64_t it = blockIdx.x; it < A.nitems; it += gridDim.x) {
+        const int k = (int)(it / A.nper);
+        int64_t r = it - (int64_t)k * A.nper;
+        // columns [64(m-1), 64m) hold m valid chunks (m < ndc), the rest ndc
+        int x = -1, c = 0;
+        for (int m = 1; m < A.ndc; m++) {
+            const int64_t n = (int64_t)max(0, min(64, A.W - 64 * (m - 1))) * m;
+            if (r < n) {
+                x = 64 * (m - 1) + (int)(r / m);
+                c = (int)(r % m);
+                break;
+            }
+            r -= n;
+        }
+        if (x < 0) {
+            x = 64 * (A.ndc - 1) + (int)(r / A.ndc);
+            c = (int)(r % A.ndc);
+        }
+        cbca_v_item<R>(A, x, c, k, sP, sN);
     }
 }
 
@@ -382,64 +438,52 @@ __global__ __launch_bounds__(64, 3) void cbca_v_kernel(const CbcaArgs A)
 // VALID_ONLY: the shear of an aggregated left volume into the right one's valid voxels (x + d <
 // W; the others untouched); s = -1 / +1 over every voxel: a right-referenced volume into left
 // coordinates and back (its invalid voxels ride on the left-coordinate invalid ones).
-// Tile = (row, 64-disparity chunk, 64 output pixels); its 127 source pixels are staged in LDS
-// (stride 64 floats: the diagonal reads hit 64 distinct banks), tiles sharing source pixels
-// sit 8 blocks apart (one XCD under round-robin dispatch: L2 reuse, speed only).
+// Tile = (row, NP output pixels, every disparity): its sources form a parallelogram -- source
+// pixel r of the tile contributes the contiguous disparities whose outputs land in the tile --
+// so every source voxel is read by exactly one tile, as runs of <= NP floats.  The tile is
+// assembled in LDS as [pixel][d] (row stride S even: the runs' diagonal writes hit distinct
+// banks, the output rows are read contiguously) and leaves as whole pixel runs.
 // ---------------------------------------------------------------------------------------------
-template <bool VEC4>
+template <int NP>
 __global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restrict__ in, float *__restrict__ out, int H,
-                                                          int W, int D, int s, int valid_only, int64_t ntiles,
-                                                          int64_t per_xcd)
+                                                          int W, int D, int S, int s, int valid_only, int64_t ntiles)
 {
-    __shared__ float buf[127 * 64];
-    const int64_t b = blockIdx.x;
-    const int64_t tile = (b % 8) * per_xcd + b / 8;
+    extern __shared__ float rbuf[];          // [NP][S]
+    const int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
-    const int nxs = (W + 63) / 64, ndc = (D + 63) / 64;
-    const int xs = (int)(tile % nxs);
-    const int64_t rem = tile / nxs;
-    const int c = (int)(rem % ndc), y = (int)(rem / ndc);
-    const int x0 = 64 * xs, d0 = 64 * c;
-    const int tid = threadIdx.x;
+    const int nxs = (W + NP - 1) / NP;
+    const int y = (int)(tile / nxs), x0 = (int)(tile % nxs) * NP;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
     const __amdgpu_buffer_rsrc_t ri = cb_rsrc(in + (size_t)y * W * D, rowbytes);
     const __amdgpu_buffer_rsrc_t ro = cb_rsrc(out + (size_t)y * W * D, rowbytes);
-    // source row r of the tile = pixel (base + r) mod W
-    const int64_t base = s > 0 ? (int64_t)x0 + d0 : (int64_t)x0 - d0 - 63;
-    auto srcpix = [&](int r) { return (int)((((base + r) % W) + W) % W); };
-    if (VEC4) {
-        // 16 lanes per 256-B run: thread t loads chunk t % 16 of rows t / 16 + 16 m
-#pragma unroll
-        for (int m = 0; m < 8; m++) {
-            const int r = tid / 16 + 16 * m;
-            if (r < 127) {
-                const int col = 4 * (tid % 16);
-                const uint32_t off = d0 + col < D ? 4u * ((uint32_t)srcpix(r) * D + d0 + col) : CB_OOB;
-                const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 0));
-                *(float4 *)&buf[r * 64 + col] = v;
-            }
-        }
-    } else {
-#pragma unroll 4
-        for (int m = 0; m < 32; m++) {
-            const int r = tid / 64 + 4 * m;
-            if (r < 127) {
-                const int col = tid % 64;
-                const uint32_t off = d0 + col < D ? 4u * ((uint32_t)srcpix(r) * D + d0 + col) : CB_OOB;
-                buf[r * 64 + col] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, off, 0, 0));
-            }
-        }
+    // piece r (0 <= r < NP + D - 1): source pixel (x0 + base + r) mod W; output pixel p of disparity d
+    // is p = r - d (s > 0) or p = r + d - (D - 1) (s < 0)
+    const int base = s > 0 ? 0 : -(D - 1);
+    const int np = NP + D - 1;
+    for (int r = wave; r < np; r += 4) {
+        const int dlo = s > 0 ? max(0, r - (NP - 1)) : max(0, D - 1 - r);
+        const int dhi = s > 0 ? min(D - 1, r) : min(D - 1, D - 1 - r + NP - 1);
+        const int d = dlo + lane;
+        const int p = s > 0 ? r - d : r + d - (D - 1);
+        const int x = x0 + p;
+        int q = (x0 + base + r) % W;
+        if (q < 0) q += W;
+        const bool ok = d <= dhi && x < W && (!valid_only || x + d < W);
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      ri, ok ? 4u * ((uint32_t)q * D + d) : CB_OOB, 0, CBCA_NT & 1 ? 2 : 0));
+        if (d <= dhi) rbuf[p * S + d] = v;
     }
     __syncthreads();
-    const int i = tid % 64, wv = tid / 64;
-    const int d = d0 + i;
-#pragma unroll 4
-    for (int p = wv; p < 64; p += 4) {
+    // output pixels x0 + p, runs of D floats; wave w takes pixels w, w + 4, ...
+    for (int p = wave; p < NP; p += 4) {
         const int x = x0 + p;
-        const int r = s > 0 ? p + i : p - i + 63;
-        const bool ok = x < W && d < D && (!valid_only || x + d < W);
-        const uint32_t off = ok ? 4u * ((uint32_t)x * D + d) : CB_OOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, buf[r * 64 + i]), ro, off, 0, 0);
+        if (x >= W) break;
+        for (int d = lane; d < D; d += 64) {
+            const bool ok = !valid_only || x + d < W;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, rbuf[p * S + d]), ro,
+                                                  ok ? 4u * ((uint32_t)x * D + d) : CB_OOB, 0, CBCA_NT & 2 ? 2 : 0);
+        }
     }
 }
 
@@ -468,12 +512,11 @@ static int cb_resident(K kernel)
 }
 
 // Balanced static schedule: the fewest items per wave that fit the resident waves, then only as
-// many waves as that needs (every wave gets the same count, so none idles while others finish).
-static void cb_schedule(CbcaArgs &A, int resident, int &grid)
+// many waves as that needs (every wave gets the same count within one, so none idles long).
+static int cb_grid(int64_t nitems, int resident)
 {
-    const int64_t per = (A.nitems + resident - 1) / resident;
-    A.per = (int)(per > 0 ? per : 1);
-    grid = (int)((A.nitems + A.per - 1) / A.per);
+    const int64_t per = std::max<int64_t>((nitems + resident - 1) / resident, 1);
+    return (int)((nitems + per - 1) / per);
 }
 
 // One left-coordinate volume: iters x (horizontal src -> tmp, vertical tmp -> src), in place.
@@ -487,21 +530,16 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
     h.ndc = (D + 63) / 64;
     CbcaArgs v = h;
     h.nseg = (W + SDE_CBCA_SEG - 1) / SDE_CBCA_SEG;
-    h.nitems = (int64_t)H * h.ndc * h.nseg;
+    h.nper = (int64_t)H * h.ndc;
+    h.nitems = h.nper * h.nseg;
     v.nseg = (H + SDE_CBCA_SEG - 1) / SDE_CBCA_SEG;
-    int64_t n = 0;
-    for (int c = 0; c < v.ndc; c++) {
-        v.chunk_first[c] = n;
-        n += (int64_t)max(W - 64 * c, 0) * v.nseg;
-    }
-    v.chunk_first[v.ndc] = n;
-    v.nitems = n;
+    v.nper = 0;
+    for (int c = 0; c < v.ndc; c++) v.nper += (int64_t)max(W - 64 * c, 0);    // columns x >= 64c
+    v.nitems = v.nper * v.nseg;
     static std::atomic<int> res_h{0}, res_v{0};
     if (!res_h.load()) res_h = cb_resident(cbca_h_kernel<R>);
     if (!res_v.load()) res_v = cb_resident(cbca_v_kernel<R>);
-    int gh = 0, gv = 0;
-    cb_schedule(h, res_h.load(), gh);
-    cb_schedule(v, res_v.load(), gv);
+    const int gh = cb_grid(h.nitems, res_h.load()), gv = cb_grid(v.nitems, res_v.load());
     h.src = cv, h.dst = tmp;
     v.src = tmp, v.dst = cv;
     for (int it = 0; it < iters; it++) {
@@ -512,13 +550,14 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
 
 static void cbca_rotate(const float *in, float *out, int H, int W, int D, int s, bool valid_only, hipStream_t st)
 {
-    const int64_t ntiles = (int64_t)H * ((D + 63) / 64) * ((W + 63) / 64);
-    const int64_t per = (ntiles + 7) / 8;
-    const int64_t grid = 8 * per;
-    if (D % 4 == 0)
-        cbca_rotate_kernel<true><<<(unsigned)grid, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles, per);
+    const int S = D + (D & 1);                      // even row stride (>= D)
+    const int np = S <= 256 ? 64 : 32;              // <= 64 KB of LDS per tile
+    const int64_t ntiles = (int64_t)H * ((W + np - 1) / np);
+    const size_t lds = (size_t)np * S * sizeof(float);
+    if (np == 64)
+        cbca_rotate_kernel<64><<<(unsigned)ntiles, 256, lds, st>>>(in, out, H, W, D, S, s, valid_only ? 1 : 0, ntiles);
     else
-        cbca_rotate_kernel<false><<<(unsigned)grid, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles, per);
+        cbca_rotate_kernel<32><<<(unsigned)ntiles, 256, lds, st>>>(in, out, H, W, D, S, s, valid_only ? 1 : 0, ntiles);
 }
 
 // Shapes the 32-bit offsets cover (refused with SDE_ERR_ARG otherwise): a row of the volume and a

@@ -764,24 +764,26 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
         }
     };
     // stores 8j .. 8j+7 of the 32 (16 L, 16 R runs), issued in the first four dot rows so they
-    // drain while the strip computes.  A row outside the image gets soffset C3_SKIPOFF: with any
-    // voffset (<= 252, or CD_OOB for lanes past nd) the sum stays below 2^32 and past the records
-    // (4 W D < 2^31), so the range check drops it -- no branch per store.
-    constexpr uint32_t C3_SKIPOFF = 0x7fffffffu;
+    // drain while the strip computes.  A row outside the image stores with voffset CD_OOB: the
+    // buffer range check compares the voffset with the records (4 W D < CD_OOB) and drops it, with
+    // or without the soffset counted in (row offsets < 2^31: the sum cannot wrap) -- one select per
+    // store, no branch.
     auto emit_store = [&](int qp, int j) {
         const int rowstep = 16 * D;                         // 4 rows of the volume, bytes
 #pragma unroll
         for (int n = 8 * j; n < 8 * j + 8 && n < NST; n++) {
             if (n < 16) {
                 const int x = qp + wave + 4 * n;
-                const uint32_t so = x < W ? (uint32_t)(((qp + wave) * D + dc) * 4 + n * rowstep) : C3_SKIPOFF;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_d, so, C3_AUX);
+                const bool in = x < W;
+                const uint32_t so = in ? (uint32_t)(((qp + wave) * D + dc) * 4 + n * rowstep) : 0u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, in ? voff_d : CD_OOB, so,
+                                                      C3_AUX);
             } else {
                 const int xr = qp - dc - 63 + 4 * (n - 16) + wave;
-                const uint32_t so = (uint32_t)xr < (uint32_t)W
-                                        ? (uint32_t)(((qp - dc - 63 + wave) * D + dc) * 4 + (n - 16) * rowstep)
-                                        : C3_SKIPOFF;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, voff_d, so, C3_AUX);
+                const bool in = (uint32_t)xr < (uint32_t)W;
+                const uint32_t so = in ? (uint32_t)(((qp - dc - 63 + wave) * D + dc) * 4 + (n - 16) * rowstep) : 0u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, in ? voff_d : CD_OOB,
+                                                      so, C3_AUX);
             }
         }
     };

@@ -773,6 +773,12 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             }
         }
     }
+    // The parked values and pixel indices cross lanes through LDS: lanes read what other lanes of the
+    // wave wrote one block earlier.  Inside the loop a read is always a whole step after the writes it
+    // depends on and the compiler does not move LDS accesses of one iteration across another's; here,
+    // right after the last writes, the ordering is made explicit (wavefront-scope release/acquire and a
+    // wave barrier: no instruction with one wave per workgroup, a scheduling fence only).
+    if (WTA && g.n > 0) wave_sync();
     if (WTA && PARK && g.n > 0) {
         // the last block's scan (its values are in buffer buf_last)
         const int buf = ((g.n - 1) / PF) & 1;

@@ -1194,7 +1194,12 @@ __global__ __launch_bounds__(64) void np_piece_kernel(const uint8_t *__restrict_
     if (lane == 0) st[4 + blockIdx.x] = sum;
 }
 
-// S = 0.0f + piece 0 + piece 1 + ... in order; STAGE 0: mean = S / n, 1: std = sqrt(S / n)
+// S = 0.0f + piece 0 + piece 1 + ... in order; STAGE 0: mean = S / n, 1: std = sqrt(S / n).
+// NumPy 2.x divides the float32 sum by the intp count in float64 and rounds once to float32 (np.mean:
+// ret.dtype.type(ret / rcount); _var: true_divide by an intp into a float32 out, and its final
+// ret / rcount), so the quotient is formed in fp64 here too.  Below 2^24 pixels this equals the
+// float32 quotient S / (float)n (fp64 has more than 2 * 24 + 2 bits: the double rounding is
+// innocuous); above it (float)n would be inexact.
 template <int STAGE>
 __global__ __launch_bounds__(64) void np_stat_kernel(float *__restrict__ scratch, int sstride, int npieces, int64_t n)
 {
@@ -1202,7 +1207,7 @@ __global__ __launch_bounds__(64) void np_stat_kernel(float *__restrict__ scratch
     float *st = scratch + (size_t)blockIdx.x * sstride;
     float S = 0.0f;
     for (int c = 0; c < npieces; c++) S += st[4 + c];
-    const float q = S / (float)n;
+    const float q = (float)((double)S / (double)n);
     st[STAGE] = STAGE == 0 ? q : sqrtf(q);
 }
 

@@ -3,10 +3,15 @@
 ``imread_gray`` reproduces ``cv2.imread(path, cv2.IMREAD_GRAYSCALE)`` for 8-bit
 images: single-channel data is returned as is; colour data is converted with
 OpenCV's fixed-point BT.601 weights ``(R*4899 + G*9617 + B*1868 + 8192) >> 14``
-(match_single.py:34-38).  Decoding uses Pillow; JPEG decoders may differ from
-OpenCV's libjpeg build in the last bit (parity unpinned for JPEG input; PNG is
-lossless and exact).  ``imwrite`` writes 8-bit grayscale PNGs like
-``cv2.imwrite(..., uint8 array)`` (match_single.py:55, match.py:90).
+(match_single.py:34-38).  JPEGs take OpenCV's own route for a grayscale read
+(match.py:48-52 reads .jpg pairs): the decoder is asked for grayscale output,
+so libjpeg emits the luma plane of a YCbCr JPEG directly (Pillow: ``draft("L")``
+before ``load()``) instead of decoding colour and converting it -- the two differ
+in the last bit wherever chroma upsampling and rounding meet.  Pillow bundles
+libjpeg(-turbo) like OpenCV; an OpenCV build with another IDCT could still
+differ (cv2 is absent here: parity unpinned for JPEG beyond the luma route).
+``imwrite`` writes 8-bit grayscale PNGs like ``cv2.imwrite(..., uint8 array)``
+(match_single.py:55, match.py:90).
 """
 from __future__ import annotations
 
@@ -22,6 +27,8 @@ def imread_gray(path: str):
         return None
     try:
         im = Image.open(path)
+        if im.format == "JPEG" and im.mode in ("RGB", "YCbCr"):
+            im.draft("L", im.size)          # libjpeg grayscale output: the luma plane, as cv2 reads it
         im.load()
     except Exception:
         return None

@@ -58,19 +58,24 @@ def pairs_for_rank(npairs: int, world: int, rank: int):
 
 
 def init_from_env(backend: str | None = None):
-    """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
+
+    backend: "nccl" (= RCCL on ROCm; one GPU per rank, cuda:LOCAL_RANK) or "gloo" (collectives on host
+    tensors, device tensors staged through host memory; ranks may share a GPU: cuda:LOCAL_RANK mod
+    the device count).  Default: the SDE_DIST_BACKEND environment variable, else nccl with a GPU and
+    gloo without -- so the multi-rank paths can be exercised as fresh processes on a one-GPU box."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend is None:
+        backend = os.environ.get("SDE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if backend not in ("nccl", "gloo"):
+        raise ValueError(f"backend must be nccl or gloo (got {backend!r})")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local if backend == "nccl" else local % torch.cuda.device_count())
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)
-    elif torch.cuda.is_available():
-        torch.cuda.set_device(local)
     return rank, world, local
 
 
@@ -147,6 +152,11 @@ class DisparityShardedMatcher:
         # a short last band writes a contiguous [2, hb, W, nf] buffer first
         self.band_out = self.band if hb == self.rpb else \
             (torch.empty((2, hb, W, nf), dtype=torch.float32, device=dev) if hb > 0 else None)
+        # the band tower's workspace is band-sized (self.m's full-image tower workspace is never
+        # allocated: StereoMatcher allocates it on first use, and only band_steps runs a tower here)
+        from . import ops
+        self.band_ws = torch.empty((max(ops.tower_batch_workspace_bytes(hb, W, 2, L, nf), 1),), dtype=torch.uint8,
+                                   device=dev) if hb > 0 else None
         self.full = torch.empty((world * 2, self.rpb, W, nf), dtype=torch.float32, device=dev)
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
 
@@ -157,7 +167,7 @@ class DisparityShardedMatcher:
         if self.band_pad is None:
             return iter(())
         self.band_pad.copy_(m.img_pad2[:, self.r0:self.r1 + 2 * L])
-        return tower_steps(self.band_pad, m.packed, L, self.band_out, m.ws, m.tower_precision, m.nf)
+        return tower_steps(self.band_pad, m.packed, L, self.band_out, self.band_ws, m.tower_precision, m.nf)
 
     def features(self):
         from . import ops

@@ -116,8 +116,7 @@ class StereoMatcher:
         self.stats = [self.stats2[:n], self.stats2[n:]]
         self.feat2 = torch.empty((2, H, W, nf), dtype=torch.float32, device=dev)
         self.feat = [self.feat2[0], self.feat2[1]]
-        nws = ops.tower_batch_workspace_bytes(H, W, 2, L, nf)
-        self.ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=dev)
+        self._ws = None        # the tower workspace, allocated on first use (see ws)
         self.disp = torch.empty((H, W), dtype=torch.float32, device=dev)
         self.min_cost = torch.empty((H, W), dtype=torch.float32, device=dev)
         self.argmin = torch.empty((H, W), dtype=torch.int32, device=dev)
@@ -132,6 +131,16 @@ class StereoMatcher:
         self.sgm_bufs = None
         if sgm:
             self._alloc_sgm()
+
+    @property
+    def ws(self):
+        """Tower workspace (both images' activations + bound words, ~4 x H x W x 64 floats), allocated
+        on first use: a matcher whose tower runs elsewhere (parallel.DisparityShardedMatcher's band
+        tower) never holds it."""
+        if self._ws is None:
+            nws = ops.tower_batch_workspace_bytes(self.H, self.W, 2, self.nlayers, self.nf)
+            self._ws = torch.empty(max(nws, 1), dtype=torch.uint8, device=self.device)
+        return self._ws
 
     # -- stages ----------------------------------------------------------------
     def load_images(self, left_u8, right_u8):

@@ -47,3 +47,27 @@ def test_multirank_classes_on_one_gpu(gpu, world, H, W, D):
     for r, (p, out) in enumerate(zip(procs, outs)):
         print(out)
         assert p.returncode == 0, f"rank {r} failed:\n{out[-3000:]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,scaling", [("pairdp", "weak"), ("dshard", "strong"), ("dshard_rep", "strong"),
+                                          ("rowband", "strong")])
+def test_bench_multirank_modes_on_one_gpu(gpu, mode, scaling):
+    """bench.py --gpus 2 exactly as the driver's scaling run launches it (torch.distributed.run, one
+    process per rank), here both ranks on the box's one GPU over gloo (SDE_DIST_BACKEND=gloo; on an
+    8-GPU node the same code runs one rank per GPU over RCCL): every mode the scaling run can use
+    must come back with one JSON line whose n_gpus, scaling and parallelism say what ran."""
+    import json
+    port = _free_port()
+    env = dict(os.environ, SDE_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mode", mode,
+           "--workload", "cones", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["config"]["parallelism"] == f"{mode}2"
+    assert line["value"] > 0 and line["steps"] == 2

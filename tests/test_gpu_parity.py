@@ -298,11 +298,14 @@ def test_tower_winograd_large_plane_takes_direct_kernel(gpu):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("H,W", [(37, 53), (1, 9), (7, 1), (375, 450), (1024, 1024), (2000, 3000), (1110, 1390)])
+@pytest.mark.parametrize("H,W", [(37, 53), (1, 9), (7, 1), (375, 450), (1024, 1024), (2000, 3000), (1110, 1390),
+                                 (4097, 4099)])
 def test_preprocess_u8(gpu, oracle, H, W):
     """Device z-norm + pad == NumPy's (I - np.mean(I)) / np.std(I) on the float32 image
     (match_single.py:40-41) bit for bit, at the configs' sizes: NumPy's float32 reduction order
-    (pairwise sums of 8192-element pieces, added in order) restated on the device."""
+    (pairwise sums of 8192-element pieces, added in order) restated on the device.  4097 x 4099 is an
+    odd count above 2^24 pixels, where NumPy 2's fp64 quotient of the sum and the count differs from
+    a float32 one (the count is not a float32)."""
     from scenedepthestimation_amd import ops
     rng = np.random.default_rng(H * 7 + W)
     img = rng.integers(0, 256, (H, W)).astype(np.uint8)

@@ -85,6 +85,25 @@ def test_imageio_cv2_gray_rule(tmp_path):
     assert imageio.imread_gray(str(tmp_path / "missing.png")) is None
 
 
+def test_imageio_jpeg_gray_is_the_luma_plane():
+    """cv2.imread(jpg, IMREAD_GRAYSCALE) has libjpeg emit a YCbCr JPEG's luma plane (match.py:48-52);
+    imread_gray must return exactly that plane -- checked against the Y channel of a raw YCbCr decode
+    of the committed fixture (tests/golden/make_jpeg.py), which the RGB -> gray route would miss."""
+    from PIL import Image
+
+    from scenedepthestimation_amd import imageio
+    path = os.path.join(os.path.dirname(__file__), "golden", "ycbcr_4x2.jpg")
+    raw = Image.open(path)
+    raw.draft("YCbCr", raw.size)
+    luma = np.asarray(raw)[..., 0]
+    got = imageio.imread_gray(path)
+    assert got.dtype == np.uint8 and got.shape == (24, 40)
+    assert np.array_equal(got, luma)
+    rgb = np.asarray(Image.open(path).convert("RGB")).astype(np.uint32)
+    via_rgb = ((rgb[..., 0] * 4899 + rgb[..., 1] * 9617 + rgb[..., 2] * 1868 + 8192) >> 14).astype(np.uint8)
+    assert (via_rgb != luma).sum() > 10          # the fixture tells the two routes apart
+
+
 def test_cli_parsers_match_reference_flags():
     from scenedepthestimation_amd import match, match_single
     a = match_single.build_parser().parse_args([])
