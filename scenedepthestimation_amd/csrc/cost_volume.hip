@@ -19,7 +19,7 @@
 // consecutive rows -> 16 distinct bank slots).  Wave w sweeps disparities
 // [16w, 16w+16) of each chunk; the fused WTA merges the 4 per-wave first-minima
 // by (value, index) at the end, which equals the sequential scan.  The GPU
-// path's L and R volumes come from one row sweep (cvlr_row_kernel, below).
+// path's L and R volumes come from one row sweep (cvlr3_kernel, below).
 #include "sde_common.h"
 #include "cv_cert.h"
 
@@ -152,259 +152,16 @@ __global__ __launch_bounds__(256) void cv64_kernel(const float *__restrict__ own
 }
 
 // ---------------------------------------------------------------------------
-// L and R volumes in one row sweep (C = 64, [H,W,D]).
-//
-// A workgroup owns one image row y and one 64-disparity chunk [dc, dc+nd) and
-// sweeps the row in 64-pixel strips q0 = 0, 64, ...  Lane (p, h) = (lane&31,
-// lane>>5) of wave w holds TWO adjacent own pixels u = q0+2p, u+1 in VGPRs and
-// the 8 disparities e..e+7 (e = dc + 16w + 8h): rows o = u+1-e-j, j = 0..8,
-// serve both pixels (pixel u+1 at d = e+j, pixel u at d = e+j-1), so 9 LDS row
-// reads feed 16 dots -- 144 B of LDS per voxel instead of 256.
-//   * other-side rows: a 128-row LDS ring of 272-B rows; a strip needs rows
-//     [q0-dc-63, q0-dc+63] and stages only its 64 new ones.  Ring slot of row
-//     x = g&127 is (x>>1) | (x&1)<<6, so the even (or odd) rows one ds_read_b128
-//     group reads land in 16 distinct 16-B bank slots with immediate offsets;
-//   * every voxel lands in a 128-row LDS ring of R rows, R[y][q-d][d] (the right
-//     volume is the left one sheared, bit for bit); a strip emits the 64 R rows
-//     it completed as full runs (lane = disparity).  Columns are XOR-swizzled by
-//     (row>>1)&31 so the 32 rows a ds_write_b32 half-wave hits use 32 banks;
-//   * the strip's own pixels are staged (coalesced) into the half of the R ring
-//     that this strip writes last, and copied to VGPRs before it does;
-//   * L[y][q][d] leaves straight from registers (32-B pieces of the runs);
-//   * a strip's global loads are issued right after the previous strip's dot
-//     loop and L stores, into registers, so their latency overlaps the R
-//     emission and the barriers.
-// Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
+// LDS-DMA helpers of the L/R volume sweep (cvlr3_kernel below).  Rounds 1-2 ran the sweep as
+// cvlr_row_kernel (register-staged, 2 workgroups per CU) and cvlr_dma_kernel (one 512-thread
+// workgroup per CU, LDS-DMA one dot loop ahead); both measured slower than cvlr3_kernel and were
+// removed in round 4 (DESIGN.md sec. 3.1 keeps their measurements).  The padded 272-B rows, the
+// 32-row DMA units (8.5 wave-instructions of 1 KiB; lane s loads chunk s % 17 of row s / 17, chunk
+// 16 the pad) and the raw barriers below are theirs.
 // ---------------------------------------------------------------------------
-#ifndef CVLR_NT
-#define CVLR_NT 0     // nontemporal L (1) / R (2) volume stores: no gain measured (1.158 -> 1.167-1.182 ms)
-#endif
-#ifndef CVLR_SKIP
-#define CVLR_SKIP 0   // profiling builds only (tools/cvlr_variants.sh): 1 L stores, 2 R stores, 4 dots, 8 loads
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr size_t CVR_RING_BYTES = (size_t)128 * CV_RSTRIDE * 16;     // other-side rows
-constexpr size_t CVR_SMEM = CVR_RING_BYTES + (size_t)128 * 64 * 4;    // + R ring
-
-__device__ __forceinline__ int cvr_slot(int g) { const int x = g & 127; return (x >> 1) | ((x & 1) << 6); }
-__device__ __forceinline__ int cvr_rword(int xr, int col) { return (xr & 127) * 64 + (col ^ ((xr >> 1) & 31)); }
-
-__global__ __launch_bounds__(256, 2) void cvlr_row_kernel(const float *__restrict__ fl,
-                                                          const float *__restrict__ fr, int H, int W, int D,
-                                                          int nchunks, float invalid, float *__restrict__ outl,
-                                                          float *__restrict__ outr)
-{
-    extern __shared__ f32x4 cvr_sm[];
-    f32x4 *ring = cvr_sm;                                                         // 128 x 17 f32x4
-    float *rring = reinterpret_cast<float *>(reinterpret_cast<char *>(cvr_sm) + CVR_RING_BYTES);  // 128 x 64
-
-    const int job = xcd_remap(blockIdx.x, gridDim.x);   // the chunks of a row share an XCD's L2
-    const int y = job / nchunks;
-    const int dc = (job - y * nchunks) * CV_DC;
-    const int nd = min(CV_DC, D - dc);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int p = lane & 31, h = lane >> 5;
-    const int e = dc + 16 * wave + 8 * h;               // this lane's first disparity
-    const bool active = e < dc + nd;                    // uniform per half-wave
-    const size_t rowvox = (size_t)y * W;
-    const f32x4 *fl4 = reinterpret_cast<const f32x4 *>(fl) + rowvox * 16;
-    const f32x4 *fr4 = reinterpret_cast<const f32x4 *>(fr) + rowvox * 16;
-    const bool vec = (D & 3) == 0 && e + 8 <= dc + nd;
-
-    const int nstrips = (W - 1 + dc + CV_TX - 1) / CV_TX + 1;   // the last strip emits R row W-1
-    f32x4 sfr[4], sown[4];
-    auto load_strip = [&](int q0) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int idx = threadIdx.x + 256 * i, c = idx & 15;
-            const int g = q0 - dc + (idx >> 4), x = q0 + (idx >> 4);
-            if (!(CVLR_SKIP & 8) && g >= 0 && g < W) sfr[i] = fr4[(size_t)g * 16 + c];
-            if (!(CVLR_SKIP & 8) && x < W) sown[i] = fl4[(size_t)x * 16 + c];
-        }
-    };
-    load_strip(0);
-    for (int k = 0; k < nstrips; k++) {
-        const int q0 = k * CV_TX;
-        // the R-ring half of rows [q0-dc, q0-dc+63]: unwritten until this strip's dot loop
-        f32x4 *ownbuf = reinterpret_cast<f32x4 *>(rring + (((q0 - dc) & 127) >> 6) * 64 * 64);
-        // [A] other-side rows [q0-dc, q0-dc+63] -> ring, own pixels [q0, q0+63] -> ownbuf
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int idx = threadIdx.x + 256 * i, c = idx & 15;
-            const int g = q0 - dc + (idx >> 4), x = q0 + (idx >> 4);
-            if (!(CVLR_SKIP & 8) && g >= 0 && g < W) ring[cvr_slot(g) * CV_RSTRIDE + c] = sfr[i];
-            if (!(CVLR_SKIP & 8) && x < W) ownbuf[(x & 63) * 16 + (c ^ ((x >> 1) & 15))] = sown[i];
-        }
-        const int u = q0 + 2 * p;
-        const bool compute = q0 < W;
-        __syncthreads();
-        // channel pairs as 2-vectors: the products and running sums are v_pk_mul_f32 /
-        // v_pk_add_f32 on aligned register pairs (each lane still rounds exactly as the scalar code)
-        f32x2 own_a[32], own_b[32];
-        if (active && compute) {
-            const f32x4 *sa = ownbuf + (u & 63) * 16, *sb = sa + 16;
-            const int sw = (u >> 1) & 15;                  // pixels u and u+1 share it
-#pragma unroll
-            for (int c = 0; c < 16; c++) {
-                const f32x4 va = sa[c ^ sw], vb = sb[c ^ sw];
-                own_a[2 * c] = va.xy; own_a[2 * c + 1] = va.zw;
-                own_b[2 * c] = vb.xy; own_b[2 * c + 1] = vb.zw;
-            }
-        }
-        __syncthreads();                                    // ownbuf is R-ring space again
-        // [B] 9 rows x 2 pixels; every cost goes to registers (L) and the R ring
-        const bool aok = u < W, bok = u + 1 < W;
-        const int obase = u + 1 - e;
-        float ca[8], cb[8];
-        if (active) {
-            if (compute && !(CVLR_SKIP & 4)) {
-#pragma unroll
-                for (int j = 0; j < 9; j++) {
-                    const int o = obase - j;
-                    const f32x4 *row = ring + cvr_slot(o) * CV_RSTRIDE;
-                    f32x2 xa[4], xb[4];     // accumulators (0,1) (2,3) (4,5) (6,7)
-#pragma unroll
-                    for (int m = 0; m < 8; m++) {
-                        const f32x4 a = row[2 * m], b = row[2 * m + 1];
-                        const f32x2 r[4] = {a.xy, a.zw, b.xy, b.zw};
-#pragma unroll
-                        for (int t = 0; t < 4; t++) {
-                            if (j <= 7) {
-                                const f32x2 pr = own_b[4 * m + t] * r[t];
-                                xb[t] = m == 0 ? pr : xb[t] + pr;
-                            }
-                            if (j >= 1) {
-                                const f32x2 pr = own_a[4 * m + t] * r[t];
-                                xa[t] = m == 0 ? pr : xa[t] + pr;
-                            }
-                        }
-                    }
-                    if (j <= 7) {
-                        const float s = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
-                                        ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
-                        cb[j] = (bok && o >= 0) ? -(0.0f + s) : invalid;
-                        rring[cvr_rword(o, e - dc + j)] = cb[j];
-                    }
-                    if (j >= 1) {
-                        const float s = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
-                                        ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
-                        ca[j - 1] = (aok && o >= 0) ? -(0.0f + s) : invalid;
-                        rring[cvr_rword(o, e - dc + j - 1)] = ca[j - 1];
-                    }
-                }
-            } else {
-                // past the row end: R's invalid fill only
-#pragma unroll
-                for (int j = 0; j < 9; j++) {
-                    if (j <= 7) rring[cvr_rword(obase - j, e - dc + j)] = invalid;
-                    if (j >= 1) rring[cvr_rword(obase - j, e - dc + j - 1)] = invalid;
-                }
-            }
-        }
-        if (active && compute && !(CVLR_SKIP & 5)) {
-            float *la = outl + (rowvox + (size_t)u) * D + e;
-            float *lb = la + D;
-            if (vec && (CVLR_NT & 1)) {
-                typedef float cv_f4 __attribute__((ext_vector_type(4)));
-                if (aok) {
-                    __builtin_nontemporal_store((cv_f4){ca[0], ca[1], ca[2], ca[3]}, reinterpret_cast<cv_f4 *>(la));
-                    __builtin_nontemporal_store((cv_f4){ca[4], ca[5], ca[6], ca[7]}, reinterpret_cast<cv_f4 *>(la) + 1);
-                }
-                if (bok) {
-                    __builtin_nontemporal_store((cv_f4){cb[0], cb[1], cb[2], cb[3]}, reinterpret_cast<cv_f4 *>(lb));
-                    __builtin_nontemporal_store((cv_f4){cb[4], cb[5], cb[6], cb[7]}, reinterpret_cast<cv_f4 *>(lb) + 1);
-                }
-            } else if (vec) {
-                if (aok) {
-                    reinterpret_cast<float4 *>(la)[0] = make_float4(ca[0], ca[1], ca[2], ca[3]);
-                    reinterpret_cast<float4 *>(la)[1] = make_float4(ca[4], ca[5], ca[6], ca[7]);
-                }
-                if (bok) {
-                    reinterpret_cast<float4 *>(lb)[0] = make_float4(cb[0], cb[1], cb[2], cb[3]);
-                    reinterpret_cast<float4 *>(lb)[1] = make_float4(cb[4], cb[5], cb[6], cb[7]);
-                }
-            } else {
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    if (e + t < dc + nd) {
-                        if (aok) la[t] = ca[t];
-                        if (bok) lb[t] = cb[t];
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (k + 1 < nstrips) load_strip(q0 + CV_TX);
-        __syncthreads();
-        // [C] emit the completed R rows x' in [q0-dc-63, q0-dc] as full runs
-        if (!(CVLR_SKIP & 2) && lane < nd) {
-            for (int t = wave; t < CV_TX; t += CV_WAVES) {
-                const int xr = q0 - dc - (CV_TX - 1) + t;
-                if (xr >= 0 && xr < W) {
-                    if (CVLR_NT & 2) __builtin_nontemporal_store(rring[cvr_rword(xr, lane)], outr + (rowvox + xr) * D + dc + lane);
-                    else outr[(rowvox + xr) * D + dc + lane] = rring[cvr_rword(xr, lane)];
-                }
-            }
-        }
-        // the next strip's [A] stages its own pixels into the R-ring half these rows occupy:
-        // every wave must be done emitting first (without this barrier a fast wave overwrote a
-        // 64-disparity run a slow wave had not emitted yet -- rare, timing dependent)
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// L and R volumes in one row sweep, LDS-DMA pipelined (C = 64, [H,W,D]) -- the default.
-//
-// The kernel above issues a strip's global loads into registers after its dot loop, so
-// their latency sits between two dot loops at 2 workgroups per CU (PMC: waves waiting
-// 52 %).  Here a 512-thread workgroup (8 waves, the whole CU's LDS) owns (row y, 64-disparity
-// chunk dc) and sweeps the row in 128-pixel strips, and everything a strip needs arrives by
-// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no VALU) issued one whole dot loop ahead:
-//   * other-side rows: two parity sub-rings of 160 rows x 272 B (even rows in one, odd in the
-//     other, so the 16 rows one ds_read_b128 group reads -- 2 apart -- sit in consecutive
-//     padded rows: 16 distinct bank slots, every chunk an immediate offset).  A strip reads
-//     rows [q0-dc-63, q0-dc+127]; the next strip's 128 new rows land in slots no reader of
-//     this strip touches (191 + 128 <= 320);
-//   * own pixels: two parity buffers of 64 padded rows, copied to VGPRs at the strip start;
-//     the next strip's are DMA'd right after that copy;
-//   * a DMA wave-instruction writes 1 KiB contiguously, so a 32-row unit (32 x 17 chunks of
-//     16 B) is 8.5 instructions whose lane s loads chunk s % 17 of row s / 17 (chunk 16 is the
-//     pad: any valid 16 B);
-//   * wave (g, dq) = (w >> 2, w & 3), lane (p, h): own pixels u = q0 + 64g + 2p, u + 1 and
-//     disparities e = dc + 16dq + 8h .. +7: rows o = u+1-e-j, j = 0..8, serve both pixels
-//     (9 LDS rows -> 16 dots, as above);
-//   * every cost lands in a 64 x 128 LDS tile T[d][pixel] (stride 129); the next strip emits
-//     the tile as full L runs L[y][x][dc..] and as the R row pieces R[y][x-d][d] it holds (an R row's 64 disparities come from at
-//     most two strips) -- lane = disparity, coalesced;
-//   * per strip: wait for the DMA + barrier; the previous strip's tile values this wave stores
-//     read into registers, the next rows' DMA, the own copy; barrier; the next own pixels'
-//     DMA, the dots, with the previous strip's stores issued between their rows.  Every global
-//     access has a whole dot loop to complete.  The DMA is inline asm (hipcc's wait insertion would
-//     otherwise drain it before every LDS read); barriers are raw s_barrier after lgkmcnt(0).
-// Voxels with q >= W are R's invalid fill; strips past the row end compute nothing.
-// ---------------------------------------------------------------------------
-#ifndef CVLR_DMA
-#define CVLR_DMA 2    // 2: cvlr3_kernel (two workgroups per CU), 1: cvlr_dma_kernel, 0: cvlr_row_kernel
-#endif
-#ifndef CD_AUX
-#define CD_AUX 0      // cache-policy bits of the volume stores
-#endif
-#ifndef CD_SKIP
-#define CD_SKIP 0     // diagnostic builds only: 1 emission stores, 2 dots, 4 in-loop DMA, 8 own copy,
-                      // 16 R stores, 32 L stores, 128 per-
-                      // workgroup s_memtime / s_memrealtime deltas into outl[2b], outl[2b+1] (clock probe)
-#endif
-constexpr int CD_NX = 128;                                // own pixels per strip
-constexpr int CD_RING = 160;                              // rows per parity sub-ring
-constexpr int CD_RB = 272;                                // bytes per padded LDS row
-constexpr size_t CD_RING_BYTES = (size_t)2 * CD_RING * CD_RB;
-constexpr size_t CD_OWN_BYTES = (size_t)2 * 64 * CD_RB;
-constexpr int CD_TS = CD_NX + 1;                          // tile stride (floats per disparity)
-// the tile (64 x CD_TS floats) + the words an R lane outside the strip may read past its end
-constexpr size_t CD_SMEM = CD_RING_BYTES + CD_OWN_BYTES + (size_t)(64 * CD_TS + 64) * 4;   // 155,392 B
+constexpr int CD_RB = 272;                                // bytes per padded LDS row (17 chunks of 16 B)
 
 __device__ __forceinline__ uint32_t cd_lds(const void *p)
 {
@@ -465,189 +222,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cd_rsrc(const void *base, uint
 
 __device__ __forceinline__ void cd_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(512, 1) void cvlr_dma_kernel(const float *__restrict__ fl,
-                                                          const float *__restrict__ fr, int H, int W, int D,
-                                                          int nchunks, float invalid, float *__restrict__ outl,
-                                                          float *__restrict__ outr)
-{
-    extern __shared__ __attribute__((aligned(16))) char cd_sm[];
-    const char *ring = cd_sm;
-    const char *own = cd_sm + CD_RING_BYTES;
-    float *T = reinterpret_cast<float *>(cd_sm + CD_RING_BYTES + CD_OWN_BYTES);
-    const uint32_t ring_l = cd_lds(ring), own_l = cd_lds(own);
-
-    const int job = xcd_remap(blockIdx.x, gridDim.x);   // the chunks of a row share an XCD's L2
-    const int y = job / nchunks;
-    const int dc = (job - y * nchunks) * CV_DC;
-    const int nd = min(CV_DC, D - dc);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g = wave >> 2, dq = wave & 3;
-    const int p = lane & 31, h = lane >> 5;
-    const int e = dc + 16 * dq + 8 * h;                 // this lane's first disparity
-    const bool active = e < dc + nd;                    // uniform per half-wave
-    const size_t rowvox = (size_t)y * W;
-    const cd_u32x4 rs_o = cd_desc(fl + rowvox * 64, (uint32_t)W * 256u);   // own pixels' feature row
-    const cd_u32x4 rs_r = cd_desc(fr + rowvox * 64, (uint32_t)W * 256u);   // other side's
-    const int nstrips = (W - 1 + dc + nd - 1) / CD_NX + 1;
-    const uint64_t clk0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memtime() : 0;
-    const uint64_t rt0 = (CD_SKIP & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
-    // row y of each volume as a buffer (the host guarantees 4 W D < CD_OOB)
-    const __amdgpu_buffer_rsrc_t rl = cd_rsrc(outl + rowvox * D, (uint32_t)W * D * 4u);
-    const __amdgpu_buffer_rsrc_t rr = cd_rsrc(outr + rowvox * D, (uint32_t)W * D * 4u);   // the last strip reaches x = W-1+dc+nd-1
-
-    // a 32-row unit of other-side rows: parity par of the 64-row block at r (a multiple of 64)
-    auto ring_unit = [&](int r, int par) {
-        int k0 = (r >> 1) % CD_RING;
-        if (k0 < 0) k0 += CD_RING;                      // a multiple of 32: the unit does not wrap
-        cd_unit(rs_r, r + par, ring_l + (uint32_t)(par * CD_RING + k0) * CD_RB, lane);
-    };
-    // a 32-pixel unit of own pixels: parity par of half hf of the strip at q
-    auto own_unit = [&](int q, int hf, int par) {
-        cd_unit(rs_o, q + 64 * hf + par, own_l + (uint32_t)(par * 64 + 32 * hf) * CD_RB, lane);
-    };
-    // the tile of the strip at qp -> L rows [qp, qp+128) and the R row pieces it holds
-    // Emission of a strip's tile: emit_load reads every value this wave stores (16 L rows, 24 R
-    // rows; one wait) into registers, so the tile is free at the next barrier; emit_store(qp, j)
-    // issues stores 5j .. 5j+4 of the 40 between the dot loop's rows.  The tile is d-major,
-    // T[d * CD_TS + pixel]: lane d's L value of row t is T[d CD_TS + t] and its R value of row i is
-    // T[d (CD_TS + 1) + i] -- one base register each and immediate offsets (8 rows apart = 32 B);
-    // an R lane outside the strip reads a neighbouring word and is not stored.  A store's offset
-    // is the lane's 4 d (past the records for d >= nd or a lane outside the strip: dropped by the
-    // range check) and the row's 4 (x D + dc) in soffset; rows outside the image are skipped.
-    float vl[16], vr[24];
-    const float *tl = T + lane * CD_TS + wave;
-    const float *tr = T + lane * (CD_TS + 1) + wave - 63;
-    const uint32_t voff_l = lane < nd ? 4u * lane : CD_OOB;
-    auto emit_load = [&]() {
-#pragma unroll
-        for (int n = 0; n < 16; n++) vl[n] = tl[8 * n];
-#pragma unroll
-        for (int n = 0; n < 24; n++) vr[n] = tr[8 * n];
-    };
-    auto emit_store = [&](int qp, int j) {
-        if (CD_SKIP & 1) return;
-#pragma unroll
-        for (int n = 5 * j; n < 5 * j + 5 && n < 40; n++) {
-            if (n < 16) {
-                const int x = qp + wave + 8 * n;
-                if (x < W && !(CD_SKIP & 32))
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vl[n]), rl, voff_l,
-                                                          (x * D + dc) * 4, CD_AUX);
-            } else {
-                const int i = wave - 63 + 8 * (n - 16), xr = qp - dc + i;
-                if (i < CD_NX && xr >= 0 && xr < W && !(CD_SKIP & 16)) {
-                    const uint32_t off = (uint32_t)(i + lane) < (uint32_t)CD_NX ? voff_l : CD_OOB;
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vr[n - 16]), rr, off,
-                                                          (xr * D + dc) * 4, CD_AUX);
-                }
-            }
-        }
-    };
-
-    // strip 0's window: rows [-dc-64, 128-dc) (3 blocks x 2 parities) and own pixels [0, 128)
-    for (int un = wave; un < 10; un += 8) {
-        if (un < 6) ring_unit(-dc - 64 + 64 * (un >> 1), un & 1);
-        else own_unit(0, (un - 6) >> 1, (un - 6) & 1);
-    }
-
-    for (int k = 0; k < nstrips; k++) {
-        const int q0 = k * CD_NX;
-        const bool more = k + 1 < nstrips;
-        // this strip's rows and own pixels (and the previous dot loop's stores: leaving those in
-        // flight with a counted vmcnt(40) measured the same, 1.09-1.13 ms)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        cd_barrier();                                       // (and the previous strip's tile)
-        if (k > 0) emit_load();
-        // the next strip's rows go to slots the previous strip's dots read
-        if (more && wave < 4 && !(CD_SKIP & 4)) ring_unit(q0 + CD_NX - dc + 64 * (wave >> 1), wave & 1);
-        const bool compute = q0 + 64 * g < W;              // wave-uniform
-        const int u = q0 + 64 * g + 2 * p;
-        // own pixels u (even buffer) and u + 1 (odd buffer), row 32g + p of each
-        f32x2 own_a[32], own_b[32];
-        if (active && compute && !(CD_SKIP & 8)) {
-            const f32x4 *sa = reinterpret_cast<const f32x4 *>(own + (size_t)(32 * g + p) * CD_RB);
-            const f32x4 *sb = reinterpret_cast<const f32x4 *>(own + (size_t)(64 + 32 * g + p) * CD_RB);
-#pragma unroll
-            for (int c = 0; c < 16; c++) {
-                const f32x4 va = sa[c], vb = sb[c];
-                own_a[2 * c] = va.xy; own_a[2 * c + 1] = va.zw;
-                own_b[2 * c] = vb.xy; own_b[2 * c + 1] = vb.zw;
-            }
-        }
-        cd_barrier();                                       // the own buffers and the tile are free
-        if (more && wave >= 4 && !(CD_SKIP & 4)) own_unit(q0 + CD_NX, (wave - 4) >> 1, wave & 1);
-        {
-            const int c0 = e - dc;
-            float *Tw = T + c0 * CD_TS + 64 * g + 2 * p;    // tile column of pixel u (u + 1: +1), disparity c0
-            const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
-            int kb = (obase >> 1) % CD_RING;
-            if (kb < 0) kb += CD_RING;
-            const bool aok = u < W, bok = u + 1 < W;
-            const bool dots = active && compute && !(CD_SKIP & 2);
-#pragma unroll
-            for (int j = 0; j < 9; j++) {
-                if (dots) {
-                    const int o = obase - j;
-                    int kj = kb - (j >> 1);
-                    if (kj < 0) kj += CD_RING;
-                    const f32x4 *row = reinterpret_cast<const f32x4 *>(
-                        ring + (size_t)(((j & 1) ? 0 : CD_RING) + kj) * CD_RB);
-                    f32x2 xa[4], xb[4];     // accumulators (0,1) (2,3) (4,5) (6,7)
-#pragma unroll
-                    for (int m = 0; m < 8; m++) {
-                        const f32x4 a = row[2 * m], b = row[2 * m + 1];
-                        const f32x2 r[4] = {a.xy, a.zw, b.xy, b.zw};
-#pragma unroll
-                        for (int t = 0; t < 4; t++) {
-                            if (j <= 7) {
-                                const f32x2 pr = own_b[4 * m + t] * r[t];
-                                xb[t] = m == 0 ? pr : xb[t] + pr;
-                            }
-                            if (j >= 1) {
-                                const f32x2 pr = own_a[4 * m + t] * r[t];
-                                xa[t] = m == 0 ? pr : xa[t] + pr;
-                            }
-                        }
-                    }
-                    if (j <= 7) {
-                        const float sm = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
-                                         ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
-                        Tw[j * CD_TS + 1] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
-                    }
-                    if (j >= 1) {
-                        const float sm = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
-                                         ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
-                        Tw[(j - 1) * CD_TS] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
-                    }
-                } else if (active && j < 8) {
-                    // past the row end: R's invalid fill only
-                    Tw[j * CD_TS] = invalid;
-                    Tw[j * CD_TS + 1] = invalid;
-                }
-                if (k > 0) emit_store(q0 - CD_NX, j);     // the previous strip's tile
-            }
-        }
-    }
-    cd_barrier();
-    emit_load();
-#pragma unroll
-    for (int j = 0; j < 8; j++) emit_store((nstrips - 1) * CD_NX, j);
-    if ((CD_SKIP & 128) && threadIdx.x == 0) {
-        outl[2 * blockIdx.x] = (float)(__builtin_amdgcn_s_memtime() - clk0);
-        outl[2 * blockIdx.x + 1] = (float)(__builtin_amdgcn_s_memrealtime() - rt0);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // L and R volumes in one row sweep, two workgroups per CU (C = 64, [H,W,D]) -- the default.
 //
-// cvlr_dma_kernel above holds the whole CU (155 KB of LDS, 8 waves in lock-step barrier phases):
-// its dot loops stop at every strip boundary while the CU waits (PMC: waves parked 37 % of their
+// Round 2's cvlr_dma_kernel held the whole CU (155 KB of LDS, 8 waves in lock-step barrier phases):
+// its dot loops stopped at every strip boundary while the CU waited (PMC: waves parked 37 % of their
 // cycles, VALU busy ~45 %).  Here a 256-thread workgroup (4 waves, one per SIMD) needs 69 KB of
 // LDS, so two independent workgroups share each CU and one's barrier phases and exposed loads
 // overlap the other's dots.  Workgroup = (row y, 64-disparity chunk dc), 64-pixel strips; the
-// exact NumPy-order arithmetic and the two-pixel blocking are cvlr_dma_kernel's, the mapping is
+// exact NumPy-order arithmetic and the two-pixel blocking are round 2's, the mapping is
 // per pixel group: wave w, lane (p, h) = (lane & 7, lane >> 3): own pixels u = q0 + 16w + 2p,
 // u + 1, disparities e = dc + 8h .. +7; rows o = u+1-e-j, j = 0..8, serve both pixels (the 16
 // lanes of a ds_read_b128 group read 12 distinct padded rows in distinct bank slots).
@@ -1305,11 +888,11 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
         if (layout == SDE_LAYOUT_DHW) {
             cv64_kernel<SDE_SIDE_LEFT, OUT_DHW><<<grid, 256, 0, st>>>(fl, fr, H, W, 0, D, D, invalid, out_left,
                                                                        nullptr, nullptr, nullptr);
-        } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT) ||
-                   (sides == SDE_SIDE_LEFT && CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB)) {
+        } else if ((int64_t)W * D * 4 < (int64_t)CD_OOB) {
             // one row sweep per (row, 64-disparity chunk) writes both volumes (the left one alone: the
             // same sweep without the right volume's stores).  The >64 KB dynamic-LDS opt-in is set for
-            // the kernel that launches, once per device.
+            // the kernel that launches, once per device.  (Rows of 2 GiB or more take the per-side
+            // kernels below.)
             const int nchunks = cdiv(D, CV_DC);
             const dim3 grid1((unsigned)(nchunks * H));
             auto opt_in = [](std::atomic<uint64_t> &done, const void *k, size_t bytes) {
@@ -1317,19 +900,16 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
                     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
                 });
             };
-            static std::atomic<uint64_t> a3l{0}, a3{0}, ad{0}, ar{0};
+            static std::atomic<uint64_t> a3l{0}, a3{0};
             if (sides == SDE_SIDE_LEFT) {
                 if (!opt_in(a3l, reinterpret_cast<const void *>(cvlr3_kernel<false>), C3_SMEM)) return SDE_ERR_LAUNCH;
                 cvlr3_kernel<false><<<grid1, 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, nullptr);
-            } else if (CVLR_DMA == 2 && (int64_t)W * D * 4 < (int64_t)CD_OOB) {
+            } else if (sides == (SDE_SIDE_LEFT | SDE_SIDE_RIGHT)) {
                 if (!opt_in(a3, reinterpret_cast<const void *>(cvlr3_kernel<true>), C3_SMEM)) return SDE_ERR_LAUNCH;
                 cvlr3_kernel<true><<<grid1, 256, C3_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
-            } else if (CVLR_DMA && (int64_t)W * D * 4 < (int64_t)CD_OOB) {
-                if (!opt_in(ad, reinterpret_cast<const void *>(cvlr_dma_kernel), CD_SMEM)) return SDE_ERR_LAUNCH;
-                cvlr_dma_kernel<<<grid1, 512, CD_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
             } else {
-                if (!opt_in(ar, reinterpret_cast<const void *>(cvlr_row_kernel), CVR_SMEM)) return SDE_ERR_LAUNCH;
-                cvlr_row_kernel<<<grid1, 256, CVR_SMEM, st>>>(fl, fr, H, W, D, nchunks, invalid, out_left, out_right);
+                cv64_kernel<SDE_SIDE_RIGHT, OUT_HWD><<<grid, 256, 0, st>>>(fr, fl, H, W, 0, D, D, invalid,
+                                                                            out_right, nullptr, nullptr, nullptr);
             }
         } else {
             if (sides & SDE_SIDE_LEFT)

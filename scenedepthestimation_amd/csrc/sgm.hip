@@ -403,9 +403,6 @@ struct Slot {
 #ifndef SGM_WALK
 #define SGM_WALK 1
 #endif
-#ifndef SGM_PAIR
-#define SGM_PAIR 0     // A/B only: ring refills two slots at a time (1 horizontal directions, 2 all): no gain
-#endif
 #ifndef SGM_EDGESEL
 #define SGM_EDGESEL 1  // D = 64 DPL kernels: the edge lanes' missing neighbours by selects, not branches
 #endif
@@ -599,11 +596,9 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     }
 
     // Every load is unconditional (steps past the end re-read a clamped pixel):
-    // a predicated load would make the ring slot a phi and force an early wait.
-    // Horizontal directions (every wave streams its own image row: 2048 streams 786 KB apart at
-    // 1024^2 x 192): SGM_PAIR refills the ring two slots at a time, so each wave's requests for
-    // two adjacent pixels reach the HBM together (the even slot's prefetch distance drops to PF - 1)
-    constexpr bool PAIRED = (SGM_PAIR == 2 || (SGM_PAIR == 1 && (DIRC == 2 || DIRC == 3))) && PF % 2 == 0;
+    // a predicated load would make the ring slot a phi and force an early wait.  (Refilling the
+    // ring two adjacent pixels at a time for the horizontal directions measured no gain in round 3
+    // and was removed.)
     Slot<DPL> ring[PF];
     Walker ahead;
     ahead.init(g, line);
@@ -761,16 +756,8 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             // the slot is refilled after its use (not hoisted above it): its registers are reused,
             // with no moves -- and waits -- at the loop back-edge
             if (SGM_FENCE) __builtin_amdgcn_sched_barrier(0);
-            if (!PAIRED) {
-                issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
-                ahead.advance(g);
-            } else if (j & 1) {
-                // two consecutive pixels' loads back to back (1.5 KB contiguous per wave at D = 192)
-                issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j - 1]);
-                ahead.advance(g);
-                issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
-                ahead.advance(g);
-            }
+            issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
+            ahead.advance(g);
         }
     }
     // The parked values and pixel indices cross lanes through LDS: lanes read what other lanes of the

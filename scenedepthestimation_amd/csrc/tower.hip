@@ -303,20 +303,8 @@ __device__ __forceinline__ void split3(float x, __bf16 &h, __bf16 &m, __bf16 &l)
     l = (__bf16)r2;
 }
 
-// Profiling builds only (tools/tower_variants.sh): TOWER_DIAG bits switch parts of the
-// persistent kernel off -- 1 stager HBM loads, 2 all stager work, 4 the MFMAs, 8 the MFMA
-// waves' LDS fragment reads, 16 the middle layers' output stores, 32 the per-c-block barriers, 64 the A-fragment reloads
-// (timing only), 256 the epilogue (timing only), 512 the staged values (loads kept; timing only); 128 writes per-workgroup s_memtime / s_memrealtime deltas over the kernel into
-// out[2 * blockIdx.x + {0, 1}] (clock check).  0 in the library.
 #ifndef XP_RING_F16
 #define XP_RING_F16 3
-#endif
-#ifndef TOWER_DIAG
-#define TOWER_DIAG 0
-#endif
-#ifndef TOWER_NT
-#define TOWER_NT 0     // nontemporal activation loads (1) / output stores (2): slower (the next layer
-                       // re-reads the outputs from cache; layer 231 -> 234 / 242 / 250 us)
 #endif
 
 constexpr int XP_TY = 16, XP_TX = 32;             // output tile
@@ -415,13 +403,8 @@ __device__ __forceinline__ float4 xp_load(const float *__restrict__ in, int Hin,
     if (y < Hin && x < Win) {
         const float4 *in4 = reinterpret_cast<const float4 *>(in);
         const size_t i = IN_CB ? (((size_t)cb * Hin + y) * Win + x) * 4 + chunk : ((size_t)y * Win + x) * 16 + cb * 4 + chunk;
-        if (TOWER_NT & 1) {
-            typedef float xp_f4 __attribute__((ext_vector_type(4)));
-            const xp_f4 t = __builtin_nontemporal_load(reinterpret_cast<const xp_f4 *>(in4) + i);
-            v = make_float4(t.x, t.y, t.z, t.w);
-        } else {
-            v = in4[i];
-        }
+        v = in4[i];   // default cache policy: nontemporal loads / stores measured slower (the next layer
+                      // re-reads the outputs from cache; round 2: layer 231 -> 234 / 242 / 250 us)
     }
     return v;
 }
@@ -462,7 +445,6 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
     // address arithmetic of all units out of the tile loop (it would pin ~40 VGPRs that the
     // MFMA waves' accumulators need)
     asm volatile("" : "+v"(st));
-    if (TOWER_DIAG & 2) return;
     int img, ty0, tx0;
     xp_tile(bt, t, img, ty0, tx0);
     in += img * bt.in_stride;
@@ -489,8 +471,7 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
 #pragma unroll
             for (int i = 0; i < HB; i++) {
                 const int u = st + (b0 + i) * XP_STAGERS;
-                if (TOWER_DIAG & 1) v[i] = make_float4(u * 1e-3f, 0.5f, 0.25f, (float)cb);
-                else v[i] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[i] = u < XP_UNITS ? xp_load<IN_CB>(in, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int i = 0; i < HB; i++) {
@@ -571,7 +552,7 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
 #pragma unroll 1
         for (int i = 0; i < nsteps; i++) {
             if (i + 1 < nsteps) fill(i + 1);
-            if (!(TOWER_DIAG & 32)) __syncthreads();
+            __syncthreads();
         }
         return;
     }
@@ -583,14 +564,12 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
 #pragma unroll
         for (int k = 0; k < XP_UPT; k++) {
             const int u = st + k * XP_STAGERS;
-            if (TOWER_DIAG & 1) v[k] = make_float4(u * 1e-3f, 0.5f, 0.25f, (float)cb);
-            else v[k] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[k] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb, u) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     int sc_img = -1;
     float s = 1.0f, unscale = 1.0f;
     auto store = [&](const float4 (&v)[XP_UPT], int i) {
-        if (TOWER_DIAG & 2) return;
         const int im = (tile0 + (i / XP_NCB) * gstride) / bt.tiles_img;
         if (F16 && im != sc_img) {   // the tile's image changed: its bound word (tiles run image-major)
             xp_scales(false, in_amax + im * bt.amax_stride, hdr, s, unscale);
@@ -600,17 +579,11 @@ __device__ __forceinline__ void xp_stager_loop(char *xsm, const float *__restric
 #pragma unroll
         for (int k = 0; k < XP_UPT; k++) {
             const int u = st + k * XP_STAGERS;
-            if (TOWER_DIAG & 512) {   // timing only: the loads are made, their values replaced
-                float4 c = v[k];
-                asm volatile("" : "+v"(c.x), "+v"(c.y), "+v"(c.z), "+v"(c.w));
-                if (u < XP_UNITS) xp_store<F16>(sb, u, make_float4(u * 1e-3f, 0.5f, 0.25f, c.x * 0.f), s);
-                continue;
-            }
             if (u < XP_UNITS) xp_store<F16>(sb, u, v[k], s);
         }
     };
     auto sync_step = [&](int) {
-        if (!(TOWER_DIAG & 32)) __syncthreads();
+        __syncthreads();
     };
     float4 ra[XP_UPT], rb[XP_UPT];
     load(ra, 0);
@@ -657,8 +630,7 @@ __device__ __forceinline__ XpB xp_bfrag(const char *b)
     XpB f;
 #pragma unroll
     for (int q = 0; q < NP; q++)
-        f.p[q] = (TOWER_DIAG & 8) ? __builtin_bit_cast(bf16x8, make_uint4((uint32_t)(uintptr_t)b, q, 1u, 2u))
-                                  : __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(b + 2 * q * XP_PLANE));
+        f.p[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(b + 2 * q * XP_PLANE));
     return f;
 }
 
@@ -684,8 +656,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xp_rsrc(const void *base)
 
 __device__ __forceinline__ void xp_st4(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
 {
-    if (TOWER_DIAG & 16) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(vo), "s"(so));
-    else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, (TOWER_NT & 2) ? 2 : 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
 }
 
 // One c-block for one MFMA wave: 9 taps x 4 output rows = 36 row-steps; each step's B
@@ -720,8 +691,7 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
 #pragma unroll
                 for (int k = 0; k + 1 < AL; k++) an[k][m] = an[k + 1][m];
                 const int t2 = tap + AL;
-                if (TOWER_DIAG & 64) an[AL - 1][m] = a[m];
-                else an[AL - 1][m] = t2 < 9 ? xp_afrag<NP>(wf, mt0 + m, cb, t2, lane)
+                an[AL - 1][m] = t2 < 9 ? xp_afrag<NP>(wf, mt0 + m, cb, t2, lane)
                                             : xp_afrag<NP>(wf, mt0 + m, ncb, t2 - 9, lane);
             }
         }
@@ -730,10 +700,7 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
 #pragma unroll
         for (int m = 0; m < MW; m++) {
             floatx16 &c = acc[m * XP_WROWS + r];
-            if (TOWER_DIAG & 4) {
-#pragma unroll
-                for (int q = 0; q < NP; q++) asm volatile("" ::"v"(b.p[q]), "v"(a[m].p[q]));   // keep the fragments live
-            } else if (F16) {
+            if (F16) {
                 c = mfma_h(a[m].p[1], b.p[0], c);
                 c = mfma_h(a[m].p[0], b.p[1], c);
                 c = mfma_h(a[m].p[0], b.p[0], c);
@@ -754,8 +721,7 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
         a[m] = an[0][m];
 #pragma unroll
         for (int k = 0; k + 1 < AL; k++) an[k][m] = an[k + 1][m];
-        if (TOWER_DIAG & 64) an[AL - 1][m] = a[m];
-        else an[AL - 1][m] = xp_afrag<NP>(wf, mt0 + m, ncb, AL, lane);
+        an[AL - 1][m] = xp_afrag<NP>(wf, mt0 + m, ncb, AL, lane);
     }
 }
 
@@ -792,8 +758,6 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
     int tile = blockIdx.x;
     if (tile >= bt.ntiles) return;
-    const uint64_t t_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memtime() : 0;
-    const uint64_t r_start = (TOWER_DIAG & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
     const float *hdr = wkblob + LK_F16 + LK_W;
     // F16 scalings of a tile (per image: each image has its own bound words; re-read only when
     // the tile's image changes -- tiles run image-major)
@@ -848,10 +812,7 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         for (int cb = 0; cb < XP_NCB; cb++) {
             const int ncb = (cb + 1) & (XP_NCB - 1);
             xp_cblock<F16, XP_WROWS>(acc, a, an, wf, mt0, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
-            if ((TOWER_DIAG & 256) && cb == XP_NCB - 1) {   // timing only: no epilogue, accumulators kept live
-#pragma unroll
-                for (int r = 0; r < XP_ACC; r++) asm volatile("" ::"v"(acc[r]));
-            } else if (cb == XP_NCB - 1) {
+            if (cb == XP_NCB - 1) {
                 // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
                 // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
                 // opaque copies of the lane coordinates: keep the epilogue's bias loads and
@@ -1009,27 +970,17 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                     }
                 }
             }
-            if (!(TOWER_DIAG & 32)) __syncthreads();
+            __syncthreads();
             cur ^= 1;
         }
     }
     if (F16 && !LAST) flush_amax();
-    if ((TOWER_DIAG & 128) && tid == 0) {
-        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        out[2 * blockIdx.x] = (float)(t1 - t_start);
-        out[2 * blockIdx.x + 1] = (float)(r1 - r_start);
-    }
 }
 
 }  // namespace sde
 #include "tower_wino.h"
-#include "tower_skew.h"
 namespace sde {
 
-#ifndef TOWER_SKEW
-#define TOWER_SKEW 0     // 1: f16x3 non-last layers on conv64_skew_kernel (tower_skew.h: bit-identical, measured
-                         // slower -- 248-254 vs 233 us per layer-image, tower pair 1.80-1.84 vs 1.74-1.75 ms)
-#endif
 
 // max |x| over n floats, atomically maxed (as float bits) into *amax (F16 tower scaling):
 // float4 grid-stride loads, one atomic per workgroup.
@@ -1406,15 +1357,6 @@ static void set_tower_attrs()
     SDE_WINO_ATTR(false, false, true);
     SDE_WINO_ATTR(false, false, false);
 #undef SDE_WINO_ATTR
-#define SDE_SKEW_ATTR(F, I, O) (void)hipFuncSetAttribute((const void *)conv64_skew_kernel<F, I, O>, \
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, SK_SMEM)
-    SDE_SKEW_ATTR(true, false, true);
-    SDE_SKEW_ATTR(true, false, false);
-    SDE_SKEW_ATTR(false, true, true);
-    SDE_SKEW_ATTR(false, true, false);
-    SDE_SKEW_ATTR(false, false, true);
-    SDE_SKEW_ATTR(false, false, false);
-#undef SDE_SKEW_ATTR
     });
 }
 
@@ -1484,16 +1426,6 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         bt.pix_stride = (int64_t)hout * wout;
         bt.amax_stride = amax_stride;
         const int grid = std::min(bt.ntiles, cu_count());
-        if (TOWER_SKEW && f16 && !last) {
-            // the two M-tiles of a tile on two waves per SIMD, one c-block apart (tower_skew.h)
-#define SDE_SKEW(F, I, O) conv64_skew_kernel<F, I, O><<<grid, 768, SK_SMEM, st>>>(in, Hin, Win, (F) ? w1 : nullptr, wk, \
-                                                                               out, hout, wout, bt, in_amax, out_amax)
-            if (layer == 2) { if (out_cb) SDE_SKEW(true, false, true); else SDE_SKEW(true, false, false); }
-            else if (in_cb) { if (out_cb) SDE_SKEW(false, true, true); else SDE_SKEW(false, true, false); }
-            else { if (out_cb) SDE_SKEW(false, false, true); else SDE_SKEW(false, false, false); }
-#undef SDE_SKEW
-            return;
-        }
 #define SDE_X6P(F, L, I, O, H) conv64_x6p_kernel<F, L, I, O, H><<<grid, 512, XP_SMEM, st>>>( \
         in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
         (L) ? onrm : nullptr, bt, in_amax, out_amax)

@@ -104,6 +104,30 @@ def test_north_star_winograd_tower_vs_fp64_band(gpu, oracle):
     ref = oracle.tower_forward(pad[500:524 + 10], hw, hb)
     assert np.abs(host(mw.feat[0])[500:524] - ref).max() < 1e-5
 
+@pytest.mark.parametrize("name,H,W", [("C4", 1110, 1390), ("C3", 2000, 3000), ("C5", 3840, 2160)])
+def test_config_tower_vs_fp64_bands(gpu, oracle, name, H, W):
+    """The default f16x3 tower at the large configs' sizes (mc_cnn_brunch.py:31-48): 24-row bands of
+    both images -- one mid-image, one at the bottom edge -- against the fp64 restatement, <= 1e-5.
+    The f16x3 scalings use image-wide bound words, so these sizes are where a band check belongs."""
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    left, right, _ = stereo_pair(H, W, 64, seed=7)
+    m = StereoMatcher(H, W, 64)
+    m.load_images(left, right)
+    m.features()
+    hw, hb = _weights()
+    for i in range(2):
+        pad = host(m.img_pad[i])
+        feat = m.feat[i]
+        for r0 in (H // 2 - 12, H - 24):
+            ref = oracle.tower_forward(pad[r0:r0 + 24 + 10], hw, hb)
+            err = float(np.abs(host(feat[r0:r0 + 24]) - ref).max())
+            print(f"{name} image {i} rows {r0}..{r0 + 23}: max |f16x3 - fp64| = {err:.2e}")
+            assert err < 1e-5, (name, i, r0, err)
+    del m
+    torch.cuda.empty_cache()
+
+
 # ----------------------------------------------------------------------------
 # north star: 1024 x 1024, D = 192
 # ----------------------------------------------------------------------------

@@ -1,4 +1,6 @@
 // tower_skew.h -- f16x3 64->64 conv with the two M-tiles of a tile skewed by one c-block (gfx950).
+// NOT BUILT (round 4): measured slower than conv64_x6p_kernel (248-254 vs 233 us per layer-image), removed
+// from libsde.so; kept under tools/variants/ as the record of the experiment.
 // Included by tower.hip after conv64_x6p_kernel, whose helpers it uses (same arithmetic, same bits).
 //
 // In conv64_x6p_kernel one MFMA wave per SIMD owns 4 output rows x all 64 output channels; at the
