@@ -1,4 +1,5 @@
-"""GPU-path L/R cost volumes alone (sde_cost_volume HWD, both sides) at H W D (profiling driver)."""
+"""GPU-path cost volumes alone (sde_cost_volume HWD) at H W D (profiling driver): both sides, or the
+left one only with a fourth argument "left" (the aggregation path's sweep)."""
 import os
 import sys
 
@@ -13,6 +14,7 @@ fl = torch.from_numpy(features(H, W, seed=0)).cuda()
 fr = torch.from_numpy(features(H, W, seed=1)).cuda()
 L = torch.empty((H, W, D), device="cuda")
 R = torch.empty((H, W, D), device="cuda")
+both = not (len(sys.argv) > 4 and sys.argv[4] == "left")
 for _ in range(5):
-    ops.cost_volume(fl, fr, D, layout="HWD", right=True, invalid=1.0, out_left=L, out_right=R)
+    ops.cost_volume(fl, fr, D, layout="HWD", right=both, invalid=1.0, out_left=L, out_right=R if both else None)
 torch.cuda.synchronize()

@@ -16,11 +16,12 @@ import os
 import subprocess
 import sys
 
-KERNELS = {   # key -> (substring of the kernel name, sum over distinct names)
+KERNELS = {   # key -> (substring of the kernel name, sum over distinct names) or [(substring, dispatches per unit)]
     "tower_conv64_layer": ("conv64_x6p_kernel<false, false, true, true, true>", False),
     "cv_wta_row": ("cv_wta_row2_kernel<false>", False),
     "cvlr": ("cvlr3_kernel", False),
-    "cbca_pair_iteration": ("cbca_scan_kernel", True),
+    # one sde_cbca_lr call at 2 iterations: 2 transposes, 2 x (horizontal + vertical pass), 1 shear
+    "cbca_lr": [("cbca_transpose_kernel", 2), ("cbca_h_kernel", 2), ("cbca_v_kernel", 2), ("cbca_rotate_kernel", 1)],
     "sgm_pair": ("sgm_scan_kernel", True),
 }
 WORKLOAD_KEYS = {"north_star": "tower_conv64_layer", "cones": None, "cv": "cv_wta_row",
@@ -51,15 +52,19 @@ def summarise(outdir, dst):
     out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/kernels_once.py "
                      "(1024x1024, D=192); median dispatch per kernel; FETCH_SIZE KiB x 2 (gfx950 half-count of "
                      "wide reads), WRITE_SIZE KiB x 1"}
-    for key, (sub, many) in KERNELS.items():
-        names = sorted({kn for (_, kn) in med if sub in kn})
-        if not names:
+    for key, spec in KERNELS.items():
+        if isinstance(spec, list):
+            parts = [(kn, n) for sub, n in spec for kn in sorted({kn for (_, kn) in med if sub in kn})[:1]]
+            sub = " + ".join(f"{n} x {s}" for s, n in spec)
+        else:
+            sub, many = spec
+            names = sorted({kn for (_, kn) in med if sub in kn})
+            parts = [(kn, 1) for kn in (names if many else names[:1])]
+        if not parts:
             continue
-        if not many:
-            names = names[:1]
-        fetch = sum(med.get(("FETCH_SIZE", kn), (0, 0))[0] for kn in names) * 1024 * 2
-        write = sum(med.get(("WRITE_SIZE", kn), (0, 0))[0] for kn in names) * 1024
-        out[key] = {"kernel": sub, "launches": len(names), "fetch_bytes": fetch, "write_bytes": write,
+        fetch = sum(med.get(("FETCH_SIZE", kn), (0, 0))[0] * n for kn, n in parts) * 1024 * 2
+        write = sum(med.get(("WRITE_SIZE", kn), (0, 0))[0] * n for kn, n in parts) * 1024
+        out[key] = {"kernel": sub, "launches": sum(n for _, n in parts), "fetch_bytes": fetch, "write_bytes": write,
                     "traffic_bytes": fetch + write}
     for w, key in WORKLOAD_KEYS.items():
         if key and key in out:
