@@ -394,7 +394,8 @@ def main():
     rank, world, local = init_from_env()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # (init_from_env selected the device: cuda:LOCAL_RANK, or LOCAL_RANK mod the device count for
+    # ranks sharing a GPU over gloo)
     H, W, D, what = WORKLOADS[args.workload]
     left, right, _ = stereo_pair(H, W, D, seed=rank)
 

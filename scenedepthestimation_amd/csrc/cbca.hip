@@ -163,7 +163,10 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
     const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, W);
     if (t1 <= d0) return;                          // every voxel of the segment is invalid
     const int fs = max(t0 - M, d0);                // walk start = lane 0's chain base
-    const int fe = t1 - 1 + R;                     // last front position (output t1 - 1)
+    // outputs trail the front by R + 1: a step issues its output's LDS reads first (every slot they
+    // touch already holds its position -- the front's own slot still the one RS back) and consumes
+    // them after the front's work, which hides their latency
+    const int fe = t1 + R;                         // last front position (output t1 - 1)
     const uint32_t D4 = 4u * (uint32_t)D;
     const uint32_t dl4 = 4u * (uint32_t)min(d, D - 1);
     const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
@@ -184,10 +187,10 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
     // the arms first: a loop-carried register loaded after the cost prefetch would make the entry
     // path's wait for it (merged into every block start) drain the whole prefetch
     uint32_t A0, B0, A1, B1;
-    arms_blk(fs - R, A0, B0);
-    arms_blk(fs + RS - R, A1, B1);
+    arms_blk(fs - R - 1, A0, B0);
+    arms_blk(fs + RS - R - 1, A1, B1);
     // right-image arm of the trailing position, lane i = pixel t - d0 - i: the state before step fs
-    uint32_t X = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(fs - R - 1 - d0 - lane), 0, 0);
+    uint32_t X = __builtin_amdgcn_raw_buffer_load_b32(rb, 4u * (uint32_t)(fs - R - 2 - d0 - lane), 0, 0);
 #pragma unroll
     for (int j = 0; j < PF; j++)
         cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)(D4 * (uint32_t)min(fs + j, W - 1)),
@@ -195,11 +198,21 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
     double P = 0.0;
     sP[(RS - 1) * 64 + lane] = 0.0;               // P(fs - 1) = 0: read before position fs + RS - 1 lands
     // per-lane store offset of output t (4d + 4tD), advanced every step
-    uint32_t vst = 4u * (uint32_t)d + D4 * (uint32_t)(fs - R);
+    uint32_t vst = 4u * (uint32_t)d + D4 * (uint32_t)(fs - R - 1);
 
     // step j of a block at front f; CLAMP: prefetch positions may pass the row end (tail blocks)
     auto step = [&](int j, int f, uint32_t Ab, uint32_t Bb, uint32_t &sld, bool clamp) {
         const int slot = j % PF;
+        // trailing output t = f - R - 1: left-image arm (uniform) and the right-image arm chain;
+        // its prefix reads before the front's write (slot j still holds position f - RS)
+        const int t = f - R - 1;
+        const uint32_t a = ruint(Ab, j);
+        const uint32_t nb = ruint(Bb, j);
+        X = (uint32_t)__builtin_amdgcn_update_dpp((int)nb, (int)X, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- nb
+        const int hl = min(a & 255u, X & 255u), hr = min((a >> 8) & 255u, (X >> 8) & 255u);
+        const uint32_t ib = ring_slot<RS>(j - R - 1 + hr), ia = ring_slot<RS>(j - R - 2 - hl);
+        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front: the chain of this lane starts at max(t0 - M, d) >= fs
         const float cv = cr[slot];
         P += f >= d ? (double)cv : 0.0;
@@ -207,14 +220,7 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
         const uint32_t so = clamp ? D4 * (uint32_t)min(f + PF, W - 1) : sld;
         cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
         sld = opq_s(sld + D4);
-        // trailing output t = f - R: left-image arm (uniform) and the right-image arm chain
-        const int t = f - R;
-        const uint32_t a = ruint(Ab, j);
-        const uint32_t nb = ruint(Bb, j);
-        X = (uint32_t)__builtin_amdgcn_update_dpp((int)nb, (int)X, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- nb
-        const int hl = min(a & 255u, X & 255u), hr = min((a >> 8) & 255u, (X >> 8) & 255u);
-        const uint32_t ib = ring_slot<RS>(j - R + hr), ia = ring_slot<RS>(j - R - hl - 1);
-        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
         const float out = (float)(pb - pa);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, t >= th ? vst : CB_OOB, 0,
                                               CBCA_NT & 2 ? 2 : 0);
@@ -233,7 +239,7 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
 #pragma unroll
         for (int j = 0; j < RS; j++)
             if (!clamp || fb + j <= fe) step(j, fb + j, Ap, Bp, sld, clamp);
-        arms_blk(fb + 2 * RS - R, Ap, Bp);
+        arms_blk(fb + 2 * RS - R - 1, Ap, Bp);
         fb += RS;
     };
     auto full = [&]() { return fb + RS - 1 <= fe && fb + RS - 1 + PF <= W - 1; };
@@ -289,11 +295,11 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, H);
     const int fc = max(t0 - M, 0);               // chain base (every valid lane)
     const int fs = fc & ~3;                      // walk start: 16-B aligned dwordx4 of four rows
-    const int fe = t1 - 1 + R;
+    const int fe = t1 + R;                       // outputs trail the front by R + 1 (as horizontally)
     const bool lane_ok = d < D && d <= x;
     const uint32_t dl4 = 4u * (uint32_t)min(d, D - 1);
     const uint32_t rowv = 4u * (uint32_t)W * (uint32_t)D;       // one row of the volume
-    // descriptors over the column, rebased on row fbase (loads) / fb - R (stores) every block, their
+    // descriptors over the column, rebased on row fbase (loads) / fb - R - 1 (stores) every block, their
     // ranges covering the rows a block touches (< 2^31 bytes: the shape check)
     const uint32_t win = (uint32_t)(RS + PF + R + 1) * rowv;
     const __amdgpu_buffer_rsrc_t ra = cb_rsrc(A.alT + (size_t)x * Hp, 4u * (uint32_t)Hp);
@@ -329,10 +335,19 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     sP[(RS - 1) * 64 + lane] = 0.0;               // Q(fs - 1) = 0, N(fs - 1) = 0
     sN[(RS - 1) * 64 + lane] = 0;
 
-    // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R
+    // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R - 1
     auto step = [&](int j, int f, int fbase, uint32_t Ab, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rd,
                     uint32_t &sld, uint32_t &sst, bool clamp) {
         const int slot = j % PF;
+        // trailing output t = f - R - 1: its support from the ring slot of position t (the front
+        // overwrites it below), its prefix / count reads before the front's writes
+        const int t = f - R - 1;
+        const uint32_t sy = sup[j % U];
+        const int vu = sy & 0xFFFF, vd = sy >> 16;
+        const uint32_t ib = ring_slot<RS>(j - R - 1 + vd), ia = ring_slot<RS>(j - R - 2 - vu);
+        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        const uint16_t nb = sN[ib * 64 + lane], na = sN[ia * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front f: chain (rows >= fc), count contribution and vertical support
         const uint32_t a = ruint(Ab, j);
         const uint32_t bw = Bq[j / 4][j % 4];
@@ -353,13 +368,10 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         const uint32_t so = clamp ? rowv * (uint32_t)(min(f + PF, H - 1) - fbase) : sld;
         cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
         sld = opq_s(sld + rowv);
-        // trailing output t = f - R, support from the ring slot of position t
-        const int t = f - R;
-        const uint32_t sy = sup[(j + 1) % U];
-        const int vu = sy & 0xFFFF, vd = sy >> 16;
-        const uint32_t ib = ring_slot<RS>(j - R + vd), ia = ring_slot<RS>(j - R - vu - 1);
-        const double num = sP[ib * 64 + lane] - sP[ia * 64 + lane];
-        const uint32_t cnt = (uint16_t)(sN[ib * 64 + lane] - sN[ia * 64 + lane]);
+        __builtin_amdgcn_sched_barrier(0);
+        // the output (row t = f - R - 1: soffset j rows on the block's store descriptor)
+        const double num = pb - pa;
+        const uint32_t cnt = (uint16_t)(nb - na);
         const float out = (float)(num * cb_recip(cnt));
         const uint32_t vo = (lane_ok && t >= t0) ? 4u * (uint32_t)d : CB_OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, vo, (int)sst, CBCA_NT & 2 ? 2 : 0);
@@ -370,10 +382,10 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     // first two blocks peeled, two blocks per loop iteration, clamped tail blocks
     auto block = [&](uint32_t &Ap, bool clamp) {
         // loads for positions fb + PF .. go against a descriptor rebased on row fbase (a tail block
-        // may start past the last row), stores against one rebased on row fb - R
+        // may start past the last row), stores against one rebased on row fb - R - 1
         const int fbase = clamp ? min(fb, H - 1) : fb;
         const __amdgpu_buffer_rsrc_t rc = cb_rsrc(A.src + ((size_t)fbase * W + x) * D, win);
-        const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R) * W + x) * D, win);
+        const __amdgpu_buffer_rsrc_t rd = cb_rsrc(A.dst + ((size_t)(fb - R - 1) * W + x) * D, win);
         uint32_t sld = rowv * (uint32_t)PF, sst = 0;
 #pragma unroll
         for (int j = 0; j < RS; j++)
@@ -438,52 +450,78 @@ __global__ __launch_bounds__(64, 2) void cbca_v_kernel(const CbcaArgs A)
 // VALID_ONLY: the shear of an aggregated left volume into the right one's valid voxels (x + d <
 // W; the others untouched); s = -1 / +1 over every voxel: a right-referenced volume into left
 // coordinates and back (its invalid voxels ride on the left-coordinate invalid ones).
-// Tile = (row, NP output pixels, every disparity): its sources form a parallelogram -- source
-// pixel r of the tile contributes the contiguous disparities whose outputs land in the tile --
-// so every source voxel is read by exactly one tile, as runs of <= NP floats.  The tile is
-// assembled in LDS as [pixel][d] (row stride S even: the runs' diagonal writes hit distinct
-// banks, the output rows are read contiguously) and leaves as whole pixel runs.
+// Tile = (row, RT_NP output pixels, RT_ND disparities): its sources form a parallelogram --
+// source pixel r of the tile contributes the contiguous disparities whose outputs land in the
+// tile -- so every source voxel is read by exactly one tile, as runs of <= RT_ND floats.  The
+// tile is assembled in LDS as [pixel][d] (the runs' diagonal writes hit distinct banks, the
+// output rows are read contiguously) and leaves as whole 256-B runs.  16-KB tiles: ten
+// workgroups per CU, and each wave keeps its 16 loads of a batch in flight together.
 // ---------------------------------------------------------------------------------------------
-template <int NP>
+constexpr int RT_NP = 64, RT_ND = 64;
 __global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restrict__ in, float *__restrict__ out, int H,
-                                                          int W, int D, int S, int s, int valid_only, int64_t ntiles)
+                                                          int W, int D, int s, int valid_only, int64_t ntiles)
 {
-    extern __shared__ float rbuf[];          // [NP][S]
+    __shared__ float rbuf[RT_NP * RT_ND];
     const int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
-    const int nxs = (W + NP - 1) / NP;
-    const int y = (int)(tile / nxs), x0 = (int)(tile % nxs) * NP;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nxs = (W + RT_NP - 1) / RT_NP, nds = (D + RT_ND - 1) / RT_ND;
+    const int y = (int)(tile / ((int64_t)nxs * nds));
+    const int rem = (int)(tile - (int64_t)y * nxs * nds);
+    const int x0 = (rem / nds) * RT_NP, d0 = (rem % nds) * RT_ND;
+    const int nd = min(RT_ND, D - d0);
+    // wave-uniform by construction; readfirstlane lets the piece indices live in SGPRs
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
     const __amdgpu_buffer_rsrc_t ri = cb_rsrc(in + (size_t)y * W * D, rowbytes);
     const __amdgpu_buffer_rsrc_t ro = cb_rsrc(out + (size_t)y * W * D, rowbytes);
-    // piece r (0 <= r < NP + D - 1): source pixel (x0 + base + r) mod W; output pixel p of disparity d
-    // is p = r - d (s > 0) or p = r + d - (D - 1) (s < 0)
-    const int base = s > 0 ? 0 : -(D - 1);
-    const int np = NP + D - 1;
-    for (int r = wave; r < np; r += 4) {
-        const int dlo = s > 0 ? max(0, r - (NP - 1)) : max(0, D - 1 - r);
-        const int dhi = s > 0 ? min(D - 1, r) : min(D - 1, D - 1 - r + NP - 1);
-        const int d = dlo + lane;
-        const int p = s > 0 ? r - d : r + d - (D - 1);
-        const int x = x0 + p;
-        int q = (x0 + base + r) % W;
-        if (q < 0) q += W;
-        const bool ok = d <= dhi && x < W && (!valid_only || x + d < W);
-        const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                      ri, ok ? 4u * ((uint32_t)q * D + d) : CB_OOB, 0, CBCA_NT & 1 ? 2 : 0));
-        if (d <= dhi) rbuf[p * S + d] = v;
+    // piece r (0 <= r < RT_NP + nd - 1): source pixel (x0 + base + r) mod W; output pixel p of relative
+    // disparity e = d - d0 is p = r - e (s > 0) or p = r + e - (nd - 1) (s < 0)
+    const int base = s > 0 ? d0 : -d0 - (nd - 1);
+    const int np = RT_NP + nd - 1;
+    constexpr int RB = 16;        // pieces per wave in flight: a batch's loads all issue before its LDS writes
+    for (int r0 = wave; r0 < np; r0 += 4 * RB) {
+        float v[RB];
+        int at[RB];
+        // source pixel of piece r0 in [0, W) (one modulo per batch; the batch's pieces step by 4)
+        int q0 = (x0 + base + r0) % W;
+        if (q0 < 0) q0 += W;
+#pragma unroll
+        for (int b = 0; b < RB; b++) {
+            const int r = r0 + 4 * b;
+            const int elo = s > 0 ? max(0, r - (RT_NP - 1)) : max(0, nd - 1 - r);
+            const int ehi = s > 0 ? min(nd - 1, r) : min(nd - 1, nd - 1 - r + RT_NP - 1);
+            const int e = elo + lane, d = d0 + e;
+            const int p = s > 0 ? r - e : r + e - (nd - 1);
+            const int x = x0 + p;
+            int q = q0 + 4 * b;
+            while (q >= W) q -= W;                // (uniform; one compare unless W < 4 * RB)
+            const bool inr = r < np && e <= ehi;
+            const bool ok = inr && x < W && (!valid_only || x + d < W);
+            v[b] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 ri, ok ? 4u * ((uint32_t)q * D + d) : CB_OOB, 0, CBCA_NT & 1 ? 2 : 0));
+            at[b] = inr ? p * RT_ND + e : -1;
+        }
+#pragma unroll
+        for (int b = 0; b < RB; b++)
+            if (at[b] >= 0) rbuf[at[b]] = v[b];
     }
     __syncthreads();
-    // output pixels x0 + p, runs of D floats; wave w takes pixels w, w + 4, ...
-    for (int p = wave; p < NP; p += 4) {
-        const int x = x0 + p;
-        if (x >= W) break;
-        for (int d = lane; d < D; d += 64) {
-            const bool ok = !valid_only || x + d < W;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, rbuf[p * S + d]), ro,
-                                                  ok ? 4u * ((uint32_t)x * D + d) : CB_OOB, 0, CBCA_NT & 2 ? 2 : 0);
+    // output pixels x0 + p (wave w: pixels w, w + 4, ...), one run of nd floats each, WB per batch
+    constexpr int WB = 8;
+#pragma unroll
+    for (int i0 = 0; i0 < RT_NP; i0 += 4 * WB) {
+        float v[WB];
+        uint32_t vo[WB];
+#pragma unroll
+        for (int b = 0; b < WB; b++) {
+            const int p = i0 + 4 * b + wave, x = x0 + p, d = d0 + lane;
+            const bool inr = x < W && lane < nd;
+            v[b] = inr ? rbuf[p * RT_ND + lane] : 0.0f;
+            vo[b] = inr && (!valid_only || x + d < W) ? 4u * ((uint32_t)x * D + d) : CB_OOB;
         }
+#pragma unroll
+        for (int b = 0; b < WB; b++)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[b]), ro, vo[b], 0, CBCA_NT & 2 ? 2 : 0);
     }
 }
 
@@ -550,14 +588,8 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
 
 static void cbca_rotate(const float *in, float *out, int H, int W, int D, int s, bool valid_only, hipStream_t st)
 {
-    const int S = D + (D & 1);                      // even row stride (>= D)
-    const int np = S <= 256 ? 64 : 32;              // <= 64 KB of LDS per tile
-    const int64_t ntiles = (int64_t)H * ((W + np - 1) / np);
-    const size_t lds = (size_t)np * S * sizeof(float);
-    if (np == 64)
-        cbca_rotate_kernel<64><<<(unsigned)ntiles, 256, lds, st>>>(in, out, H, W, D, S, s, valid_only ? 1 : 0, ntiles);
-    else
-        cbca_rotate_kernel<32><<<(unsigned)ntiles, 256, lds, st>>>(in, out, H, W, D, S, s, valid_only ? 1 : 0, ntiles);
+    const int64_t ntiles = (int64_t)H * ((W + RT_NP - 1) / RT_NP) * ((D + RT_ND - 1) / RT_ND);
+    cbca_rotate_kernel<<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles);
 }
 
 // Shapes the 32-bit offsets cover (refused with SDE_ERR_ARG otherwise): a row of the volume and a

@@ -725,6 +725,182 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
     }
 }
 
+// Tile epilogue of one MFMA wave (output rows WR*g .., M-tiles mt0 ..): bias (+ReLU | L2-normalise),
+// stores, and (F16, !LAST) the running maximum of the stored outputs for the image's bound word
+// (one atomic per wave and image, xp_flush_amax).  unscale undoes the F16 power-of-two scalings.
+__device__ __forceinline__ void xp_flush_amax(uint32_t &amax_run, int &amax_img, int lane, float *out_amax,
+                                              int amax_stride)
+{
+    if (amax_img < 0) return;
+    uint32_t a = amax_run;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax + amax_img * amax_stride), a);
+    amax_run = 0u;
+}
+
+template <bool LAST, bool OUT_CB, bool F16, int XP_WROWS>
+__device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int lane, int g, int mt0, int img,
+                                            int ty0, int tx0, float unscale, const float4 *lbias4,
+                                            float *__restrict__ out, int Hout, int Wout, const XpBatch &bt,
+                                            uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
+                                            float *__restrict__ onrm, uint32_t &amax_run, int &amax_img,
+                                            float *__restrict__ out_amax)
+{
+    constexpr int MW = 8 / XP_WROWS;
+    // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
+    // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
+    // opaque copies of the lane coordinates: keep the epilogue's bias loads and
+    // addresses inside the loop (hoisted, they would pin registers for the whole kernel)
+    int j = lane & 31, h = lane >> 5;
+    asm volatile("" : "+v"(j), "+v"(h));
+    const int x = tx0 + j;
+    const bool xok = x < Wout;
+    const int row0 = XP_WROWS * g;   // this wave's first row in the tile
+    if (!LAST) {
+        // F16: max of this lane's stored outputs of the tile, as float bits (outputs are >= +0
+        // after the ReLU, so their bits order like their values: integer max3, no NaN quieting)
+        uint32_t amax = 0u;
+        float *const outi = out + img * bt.out_stride;
+        // OUT_CB: [cblk][h][w][16] -> one descriptor per c-block plane, at the tile's first row;
+        // else [h][w][64]
+        const uint32_t vo = xok ? (uint32_t)(x * (OUT_CB ? 64 : 256) + 16 * h) : XP_OOB;
+        const size_t HW = (size_t)Hout * Wout;
+#pragma unroll
+        for (int m = 0; m < MW; m++) {
+            float4 b4[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) b4[q] = lbias4[((mt0 + m) * 32 + 8 * q + 4 * h) >> 2];
+#pragma unroll
+            for (int qh = 0; qh < 2; qh++) {
+                const int cblk = 2 * (mt0 + m) + qh;
+                const __amdgpu_buffer_rsrc_t rs =
+                    xp_rsrc(OUT_CB ? outi + ((size_t)cblk * HW + (size_t)ty0 * Wout) * 16
+                                   : outi + (size_t)ty0 * Wout * NF);
+#pragma unroll
+                for (int r = 0; r < XP_WROWS; r++) {
+                    const floatx16 &c = acc[m * XP_WROWS + r];
+                    if (ty0 + row0 + r < Hout) {   // wave-uniform
+                        const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
+#pragma unroll
+                        for (int ql = 0; ql < 2; ql++) {
+                            const int q = 2 * qh + ql;
+                            const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+                            float o4[4];
+#pragma unroll
+                            for (int e = 0; e < 4; e++)
+                                o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]),
+                                              0.f);
+                            const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                            if (F16) {
+                                amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                                amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                            }
+                            // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
+                            xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
+                        }
+                    }
+                }
+            }
+        }
+        if (F16) {
+            if (!xok) amax = 0u;   // lanes past the output edge stored nothing
+            // one atomic per wave and image (flushed when the tiles move to the next
+            // image and at the end): every workgroup maxes into the same word
+            if (img != amax_img) {
+                xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+                amax_img = img;
+            }
+            amax_run = max(amax_run, amax);
+        }
+    } else {
+        // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm.
+        // Outputs [h][w][64] (+ bf16 planes, norm bound), descriptors at the tile's first row.
+        const size_t pix0 = (size_t)img * bt.pix_stride + (size_t)ty0 * Wout;
+        const __amdgpu_buffer_rsrc_t rs = xp_rsrc(out + pix0 * NF);
+        const uint32_t vo = xok ? (uint32_t)(x * 256 + 16 * h) : XP_OOB;
+#pragma unroll
+        for (int r = 0; r < XP_WROWS; r++) {
+            // biased value of channel m*32 + 8q + 4h + e (bias re-read from LDS per use: nothing
+            // but the accumulators stays live across the row)
+            int hr = h;
+            asm volatile("" : "+v"(hr));   // per-row opaque copy: no CSE of bias reads across rows
+            auto val4 = [&](int m, int q, float (&t)[4]) {
+                const float4 bq4 = lbias4[(m * 32 + 8 * q + 4 * hr) >> 2];
+                const float bq[4] = {bq4.x, bq4.y, bq4.z, bq4.w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float cv = acc[m * XP_WROWS + r][4 * q + e];
+                    t[e] = F16 ? fmaf(cv, unscale, bq[e]) : cv + bq[e];
+                }
+            };
+            float ss = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    float t[4];
+                    val4(m, q, t);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) ss += t[e] * t[e];
+                }
+            ss += __shfl_xor(ss, 32, 64);
+            const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+            float v[2][16];
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    float t[4];
+                    val4(m, q, t);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[m][4 * q + e] = t[e] * inv;
+                }
+            float s2 = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 2; m++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) s2 += v[m][i] * v[m][i];
+            s2 += __shfl_xor(s2, 32, 64);
+            if (ty0 + row0 + r < Hout) {   // wave-uniform
+                const uint32_t rowp = (uint32_t)((row0 + r) * Wout);   // pixels from the tile's first row
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        xp_st4(make_float4(v[m][4 * q], v[m][4 * q + 1], v[m][4 * q + 2], v[m][4 * q + 3]),
+                               rs, vo + 4u * (m * 32 + 8 * q), rowp * 256u);
+                if (ohi) {
+                    const __amdgpu_buffer_rsrc_t rh = xp_rsrc(ohi + pix0 * NF), rl = xp_rsrc(olo + pix0 * NF);
+                    const uint32_t vo2 = xok ? (uint32_t)(x * 128 + 8 * h) : XP_OOB;
+#pragma unroll
+                    for (int m = 0; m < 2; m++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            bf16x4 hv, lv;
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const float xv = v[m][4 * q + e];
+                                const __bf16 hh = (__bf16)xv;
+                                hv[e] = hh;
+                                lv[e] = (__bf16)(xv - (float)hh);
+                            }
+                            const uint32_t o2 = vo2 + 2u * (m * 32 + 8 * q);
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rh, o2, rowp * 128u, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lv), rl, o2, rowp * 128u, 0);
+                        }
+                }
+                // fp32 rounding bound of the 64-term sum
+                if (onrm) {
+                    const __amdgpu_buffer_rsrc_t rn = xp_rsrc(onrm + pix0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sqrtf(s2) * 1.000004f), rn,
+                                                          (xok && h == 0) ? (uint32_t)(x * 4) : XP_OOB, rowp * 4u, 0);
+                }
+            }
+        }
+    }
+}
+
 template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB, bool F16>
 __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ w1blob,
@@ -792,14 +968,6 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
     uint32_t amax_run = 0u;
     int amax_img = -1;
-    auto flush_amax = [&]() {
-        if (amax_img < 0) return;
-        uint32_t a = amax_run;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
-        if (lane == 0) atomicMax(reinterpret_cast<unsigned int *>(out_amax + amax_img * bt.amax_stride), a);
-        amax_run = 0u;
-    };
     int cur = 0;
     for (; tile < bt.ntiles; tile += gridDim.x) {
         int img, ty0, tx0;
@@ -813,168 +981,19 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
             const int ncb = (cb + 1) & (XP_NCB - 1);
             xp_cblock<F16, XP_WROWS>(acc, a, an, wf, mt0, cb, ncb, lane, xsm + cur * XP_STAGE + bbase);
             if (cb == XP_NCB - 1) {
-                // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
-                // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
-                // opaque copies of the lane coordinates: keep the epilogue's bias loads and
-                // addresses inside the loop (hoisted, they would pin registers for the whole kernel)
-                int j = lane & 31, h = lane >> 5;
-                asm volatile("" : "+v"(j), "+v"(h));
                 float unscale = 1.0f;
-                if (F16) {   // undo the power-of-two scalings (exact)
+                if (F16) {
                     float s_unused;
                     scales(tile, s_unused, unscale);
                 }
-                const int x = tx0 + j;
-                const bool xok = x < Wout;
-                const int row0 = XP_WROWS * g;   // this wave's first row in the tile
-                if (!LAST) {
-                    // F16: max of this lane's stored outputs of the tile, as float bits (outputs are >= +0
-                    // after the ReLU, so their bits order like their values: integer max3, no NaN quieting)
-                    uint32_t amax = 0u;
-                    float *const outi = out + img * bt.out_stride;
-                    // OUT_CB: [cblk][h][w][16] -> one descriptor per c-block plane, at the tile's first row;
-                    // else [h][w][64]
-                    const uint32_t vo = xok ? (uint32_t)(x * (OUT_CB ? 64 : 256) + 16 * h) : XP_OOB;
-                    const size_t HW = (size_t)Hout * Wout;
-#pragma unroll
-                    for (int m = 0; m < MW; m++) {
-                        float4 b4[4];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) b4[q] = lbias4[((mt0 + m) * 32 + 8 * q + 4 * h) >> 2];
-#pragma unroll
-                        for (int qh = 0; qh < 2; qh++) {
-                            const int cblk = 2 * (mt0 + m) + qh;
-                            const __amdgpu_buffer_rsrc_t rs =
-                                xp_rsrc(OUT_CB ? outi + ((size_t)cblk * HW + (size_t)ty0 * Wout) * 16
-                                               : outi + (size_t)ty0 * Wout * NF);
-#pragma unroll
-                            for (int r = 0; r < XP_WROWS; r++) {
-                                const floatx16 &c = acc[m * XP_WROWS + r];
-                                if (ty0 + row0 + r < Hout) {   // wave-uniform
-                                    const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
-#pragma unroll
-                                    for (int ql = 0; ql < 2; ql++) {
-                                        const int q = 2 * qh + ql;
-                                        const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
-                                        float o4[4];
-#pragma unroll
-                                        for (int e = 0; e < 4; e++)
-                                            o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]),
-                                                          0.f);
-                                        const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
-                                        if (F16) {
-                                            amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
-                                            amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
-                                        }
-                                        // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
-                                        xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    if (F16) {
-                        if (!xok) amax = 0u;   // lanes past the output edge stored nothing
-                        // one atomic per wave and image (flushed when the tiles move to the next
-                        // image and at the end): every workgroup maxes into the same word
-                        if (img != amax_img) {
-                            flush_amax();
-                            amax_img = img;
-                        }
-                        amax_run = max(amax_run, amax);
-                    }
-                } else {
-                    // a pixel's 64 channels live in this wave (two lanes): wave-local L2 norm.
-                    // Outputs [h][w][64] (+ bf16 planes, norm bound), descriptors at the tile's first row.
-                    const size_t pix0 = (size_t)img * bt.pix_stride + (size_t)ty0 * Wout;
-                    const __amdgpu_buffer_rsrc_t rs = xp_rsrc(out + pix0 * NF);
-                    const uint32_t vo = xok ? (uint32_t)(x * 256 + 16 * h) : XP_OOB;
-#pragma unroll
-                    for (int r = 0; r < XP_WROWS; r++) {
-                        // biased value of channel m*32 + 8q + 4h + e (bias re-read from LDS per use: nothing
-                        // but the accumulators stays live across the row)
-                        int hr = h;
-                        asm volatile("" : "+v"(hr));   // per-row opaque copy: no CSE of bias reads across rows
-                        auto val4 = [&](int m, int q, float (&t)[4]) {
-                            const float4 bq4 = lbias4[(m * 32 + 8 * q + 4 * hr) >> 2];
-                            const float bq[4] = {bq4.x, bq4.y, bq4.z, bq4.w};
-#pragma unroll
-                            for (int e = 0; e < 4; e++) {
-                                const float cv = acc[m * XP_WROWS + r][4 * q + e];
-                                t[e] = F16 ? fmaf(cv, unscale, bq[e]) : cv + bq[e];
-                            }
-                        };
-                        float ss = 0.0f;
-#pragma unroll
-                        for (int m = 0; m < 2; m++)
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                float t[4];
-                                val4(m, q, t);
-#pragma unroll
-                                for (int e = 0; e < 4; e++) ss += t[e] * t[e];
-                            }
-                        ss += __shfl_xor(ss, 32, 64);
-                        const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-                        float v[2][16];
-#pragma unroll
-                        for (int m = 0; m < 2; m++)
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                float t[4];
-                                val4(m, q, t);
-#pragma unroll
-                                for (int e = 0; e < 4; e++) v[m][4 * q + e] = t[e] * inv;
-                            }
-                        float s2 = 0.0f;
-#pragma unroll
-                        for (int m = 0; m < 2; m++)
-#pragma unroll
-                            for (int i = 0; i < 16; i++) s2 += v[m][i] * v[m][i];
-                        s2 += __shfl_xor(s2, 32, 64);
-                        if (ty0 + row0 + r < Hout) {   // wave-uniform
-                            const uint32_t rowp = (uint32_t)((row0 + r) * Wout);   // pixels from the tile's first row
-#pragma unroll
-                            for (int m = 0; m < 2; m++)
-#pragma unroll
-                                for (int q = 0; q < 4; q++)
-                                    xp_st4(make_float4(v[m][4 * q], v[m][4 * q + 1], v[m][4 * q + 2], v[m][4 * q + 3]),
-                                           rs, vo + 4u * (m * 32 + 8 * q), rowp * 256u);
-                            if (ohi) {
-                                const __amdgpu_buffer_rsrc_t rh = xp_rsrc(ohi + pix0 * NF), rl = xp_rsrc(olo + pix0 * NF);
-                                const uint32_t vo2 = xok ? (uint32_t)(x * 128 + 8 * h) : XP_OOB;
-#pragma unroll
-                                for (int m = 0; m < 2; m++)
-#pragma unroll
-                                    for (int q = 0; q < 4; q++) {
-                                        bf16x4 hv, lv;
-#pragma unroll
-                                        for (int e = 0; e < 4; e++) {
-                                            const float xv = v[m][4 * q + e];
-                                            const __bf16 hh = (__bf16)xv;
-                                            hv[e] = hh;
-                                            lv[e] = (__bf16)(xv - (float)hh);
-                                        }
-                                        const uint32_t o2 = vo2 + 2u * (m * 32 + 8 * q);
-                                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rh, o2, rowp * 128u, 0);
-                                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lv), rl, o2, rowp * 128u, 0);
-                                    }
-                            }
-                            // fp32 rounding bound of the 64-term sum
-                            if (onrm) {
-                                const __amdgpu_buffer_rsrc_t rn = xp_rsrc(onrm + pix0);
-                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sqrtf(s2) * 1.000004f), rn,
-                                                                      (xok && h == 0) ? (uint32_t)(x * 4) : XP_OOB, rowp * 4u, 0);
-                            }
-                        }
-                    }
-                }
+                xp_epilogue<LAST, OUT_CB, F16, XP_WROWS>(acc, lane, g, mt0, img, ty0, tx0, unscale, lbias4, out, Hout,
+                                                         Wout, bt, ohi, olo, onrm, amax_run, amax_img, out_amax);
             }
             __syncthreads();
             cur ^= 1;
         }
     }
-    if (F16 && !LAST) flush_amax();
+    if (F16 && !LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
 }
 
 }  // namespace sde

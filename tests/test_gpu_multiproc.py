@@ -64,7 +64,9 @@ def test_bench_multirank_modes_on_one_gpu(gpu, mode, scaling):
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mode", mode,
            "--workload", "cones", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    if p.returncode != 0:
+        print(p.stdout[-3000:], "\n---- stderr ----\n", "\n".join(l for l in p.stderr.splitlines() if "Gloo" not in l)[-6000:])
+    assert p.returncode == 0, "bench.py --gpus 2 failed (output above)"
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
