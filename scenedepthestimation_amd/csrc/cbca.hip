@@ -153,11 +153,13 @@ __device__ __forceinline__ uint32_t opq_v(uint32_t v)
 // Horizontal pass: item = (segment k, row y, chunk c), c fastest; wave w takes items w, w + G, ...,
 // so the waves in flight walk the same segment of consecutive rows, a pixel's chunks side by side.
 // ---------------------------------------------------------------------------------------------
-template <int R>
+// SEL: some lane's chain starts inside the walk (d > fs: early segments); otherwise every front
+// position is on every lane's chain and the per-step select goes
+template <int R, bool SEL>
 __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int k, double *__restrict__ sP)
 {
     constexpr int RS = 2 * R + 2, PF = RS;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int W = A.W, D = A.D, M = A.M;
     const int d0 = 64 * c, d = d0 + lane;
     const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, W);
@@ -215,7 +217,7 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
         __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front: the chain of this lane starts at max(t0 - M, d) >= fs
         const float cv = cr[slot];
-        P += f >= d ? (double)cv : 0.0;
+        P += (!SEL || f >= d) ? (double)cv : 0.0;
         sP[j * 64 + lane] = P;
         const uint32_t so = clamp ? D4 * (uint32_t)min(f + PF, W - 1) : sld;
         cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
@@ -274,9 +276,23 @@ __global__ __launch_bounds__(64, 3) void cbca_h_kernel(const CbcaArgs A)
     for (int64_t it = blockIdx.x; it < A.nitems; it += gridDim.x) {
         const int k = (int)(it / A.nper);
         const int64_t r = it - (int64_t)k * A.nper;
-        cbca_h_item<R>(A, (int)(r / A.ndc), (int)(r % A.ndc), k, sP);
+        const int c = (int)(r % A.ndc);
+        if (k * SDE_CBCA_SEG - A.M >= 64 * c + 63)    // fs = max(t0 - M, d0) >= every lane's d
+            cbca_h_item<R, false>(A, (int)(r / A.ndc), c, k, sP);
+        else
+            cbca_h_item<R, true>(A, (int)(r / A.ndc), c, k, sP);
     }
 }
+
+// Vertical-pass launch shape: WPB waves per workgroup, each with its own items and LDS rings; R = 13
+// (L1 <= 14) adds a workgroup-shared table of the exact reciprocals 1/c, c <= (2R+1)^2 (one LDS
+// read per voxel for the v_rcp_f64 + Newton chain; 4 waves x 17.5 KB + 5.7 KB: still two workgroups
+// = 8 waves per CU).
+template <int R> struct CbV {
+    static constexpr int WPB = R == 13 ? 4 : 1;
+    static constexpr bool TAB = R == 13;
+    static constexpr int NT = TAB ? (2 * R + 1) * (2 * R + 1) + 1 : 1;
+};
 
 // ---------------------------------------------------------------------------------------------
 // Vertical pass: item = (segment k, column x, chunk c <= x / 64), c fastest (only chunks with a
@@ -285,11 +301,11 @@ __global__ __launch_bounds__(64, 3) void cbca_h_kernel(const CbcaArgs A)
 // ---------------------------------------------------------------------------------------------
 template <int R>
 __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, double *__restrict__ sP,
-                                            uint16_t *__restrict__ sN)
+                                            uint16_t *__restrict__ sN, const double *__restrict__ tab)
 {
     constexpr int RS = 2 * R + 2, PF = RS, U = R + 1, NQ = RS / 4;
     static_assert(RS % 4 == 0 && RS % U == 0, "ring sizes");
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int H = A.H, W = A.W, D = A.D, M = A.M, Hp = A.Hp;
     const int d0 = 64 * c, d = d0 + lane;
     const int t0 = k * SDE_CBCA_SEG, t1 = min(t0 + SDE_CBCA_SEG, H);
@@ -336,8 +352,9 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     sN[(RS - 1) * 64 + lane] = 0;
 
     // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R - 1
+    // PRE: the walk's first block (its first fc - fs <= 3 positions precede the chain)
     auto step = [&](int j, int f, int fbase, uint32_t Ab, __amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rd,
-                    uint32_t &sld, uint32_t &sst, bool clamp) {
+                    uint32_t &sld, uint32_t &sst, bool clamp, bool pre) {
         const int slot = j % PF;
         // trailing output t = f - R - 1: its support from the ring slot of position t (the front
         // overwrites it below), its prefix / count reads before the front's writes
@@ -358,7 +375,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
                                                                                     __builtin_bit_cast(u16x2, b02)));
         const uint32_t m13 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a13),
                                                                                     __builtin_bit_cast(u16x2, b13)));
-        const bool on = f >= fc;
+        const bool on = !pre || f >= fc;
         P += on ? (double)cr[slot] : 0.0;
         N += on ? ((m02 + m13) & 0xFFFFu) + 1u : 0u;
         sP[j * 64 + lane] = P;
@@ -372,7 +389,9 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         // the output (row t = f - R - 1: soffset j rows on the block's store descriptor)
         const double num = pb - pa;
         const uint32_t cnt = (uint16_t)(nb - na);
-        const float out = (float)(num * cb_recip(cnt));
+        // (an invalid lane's count may be anything: clamped into the table)
+        const double rcp = CbV<R>::TAB ? tab[min(cnt, (uint32_t)CbV<R>::NT - 1)] : cb_recip(cnt);
+        const float out = (float)(num * rcp);
         const uint32_t vo = (lane_ok && t >= t0) ? 4u * (uint32_t)d : CB_OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, vo, (int)sst, CBCA_NT & 2 ? 2 : 0);
         sst = opq_s(sst + rowv);
@@ -380,7 +399,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     int fb = fs;
     // blocks as in the horizontal pass: two alternating left-arm registers reloaded in place, the
     // first two blocks peeled, two blocks per loop iteration, clamped tail blocks
-    auto block = [&](uint32_t &Ap, bool clamp) {
+    auto block = [&](uint32_t &Ap, bool clamp, bool pre) {
         // loads for positions fb + PF .. go against a descriptor rebased on row fbase (a tail block
         // may start past the last row), stores against one rebased on row fb - R - 1
         const int fbase = clamp ? min(fb, H - 1) : fb;
@@ -389,41 +408,48 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         uint32_t sld = rowv * (uint32_t)PF, sst = 0;
 #pragma unroll
         for (int j = 0; j < RS; j++)
-            if (!clamp || fb + j <= fe) step(j, fb + j, fbase, Ap, rc, rd, sld, sst, clamp);
+            if (!clamp || fb + j <= fe) step(j, fb + j, fbase, Ap, rc, rd, sld, sst, clamp, pre);
         Ap = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fb + 2 * RS + lane), 0, 0);
         fb += RS;
     };
     auto full = [&]() { return fb + RS - 1 <= fe && fb + RS - 1 + PF <= H - 1; };
     bool odd = false;
     if (full()) {
-        block(A0, false);
+        block(A0, false, true);
         odd = true;
         if (full()) {
-            block(A1, false);
+            block(A1, false, false);
             odd = false;
             while (full()) {
-                block(A0, false);
+                block(A0, false, false);
                 if (!full()) {
                     odd = true;
                     break;
                 }
-                block(A1, false);
+                block(A1, false, false);
             }
         }
     }
     while (fb <= fe) {
-        if (odd) block(A1, true);
-        else block(A0, true);
+        if (odd) block(A1, true, fb == fs);
+        else block(A0, true, fb == fs);
         odd = !odd;
     }
 }
 
 template <int R>
-__global__ __launch_bounds__(64, 2) void cbca_v_kernel(const CbcaArgs A)
+__global__ __launch_bounds__(64 * CbV<R>::WPB, 2) void cbca_v_kernel(const CbcaArgs A)
 {
-    __shared__ double sP[(2 * R + 2) * 64];
-    __shared__ uint16_t sN[(2 * R + 2) * 64];
-    for (int64_t it = blockIdx.x; it < A.nitems; it += gridDim.x) {
+    constexpr int WPB = CbV<R>::WPB;
+    __shared__ double sP[WPB][(2 * R + 2) * 64];
+    __shared__ uint16_t sN[WPB][(2 * R + 2) * 64];
+    __shared__ double tab[CbV<R>::NT];
+    const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    if (CbV<R>::TAB) {
+        for (int c = threadIdx.x; c < CbV<R>::NT; c += 64 * WPB) tab[c] = cb_recip((uint32_t)max(c, 1));
+        __syncthreads();
+    }
+    for (int64_t it = (int64_t)blockIdx.x * WPB + wave; it < A.nitems; it += (int64_t)gridDim.x * WPB) {
         const int k = (int)(it / A.nper);
         int64_t r = it - (int64_t)k * A.nper;
         // columns [64(m-1), 64m) hold m valid chunks (m < ndc), the rest ndc
@@ -441,7 +467,7 @@ __global__ __launch_bounds__(64, 2) void cbca_v_kernel(const CbcaArgs A)
             x = 64 * (A.ndc - 1) + (int)(r / A.ndc);
             c = (int)(r % A.ndc);
         }
-        cbca_v_item<R>(A, x, c, k, sP, sN);
+        cbca_v_item<R>(A, x, c, k, sP[wave], sN[wave], tab);
     }
 }
 
@@ -538,14 +564,14 @@ static inline int cb_hp(int H) { return (H + 3) & ~3; }
 
 static size_t cbca_ws_bytes(int H, int W) { return 2 * sizeof(uint32_t) * (size_t)cb_hp(H) * (size_t)W; }
 
-// Resident one-wave workgroups of a pass kernel (occupancy x CUs), per device and kernel.
+// Resident workgroups of a pass kernel (occupancy x CUs), per device and kernel.
 template <typename K>
-static int cb_resident(K kernel)
+static int cb_resident(K kernel, int threads = 64)
 {
     int dev = 0, cus = 256, per = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, 0) != hipSuccess || per <= 0) per = 8;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per <= 0) per = 8;
     return per * cus;
 }
 
@@ -576,13 +602,15 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
     v.nitems = v.nper * v.nseg;
     static std::atomic<int> res_h{0}, res_v{0};
     if (!res_h.load()) res_h = cb_resident(cbca_h_kernel<R>);
-    if (!res_v.load()) res_v = cb_resident(cbca_v_kernel<R>);
-    const int gh = cb_grid(h.nitems, res_h.load()), gv = cb_grid(v.nitems, res_v.load());
+    if (!res_v.load()) res_v = cb_resident(cbca_v_kernel<R>, 64 * CbV<R>::WPB);   // workgroups
+    constexpr int VW = CbV<R>::WPB;
+    const int gh = cb_grid(h.nitems, res_h.load());
+    const int gv = (cb_grid(v.nitems, res_v.load() * VW) + VW - 1) / VW;   // waves -> workgroups
     h.src = cv, h.dst = tmp;
     v.src = tmp, v.dst = cv;
     for (int it = 0; it < iters; it++) {
         if (h.nitems > 0) cbca_h_kernel<R><<<gh, 64, 0, st>>>(h);
-        if (v.nitems > 0) cbca_v_kernel<R><<<gv, 64, 0, st>>>(v);
+        if (v.nitems > 0) cbca_v_kernel<R><<<gv, 64 * VW, 0, st>>>(v);
     }
 }
 
