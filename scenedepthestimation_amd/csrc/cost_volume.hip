@@ -251,15 +251,8 @@ __device__ __forceinline__ void cd_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 //     the next own pixels' DMA, dots, barrier, the next rows' DMA.
 // Voxels with x >= W are R's invalid fill; strips past the row end compute nothing.
 // ---------------------------------------------------------------------------
-#ifndef C3_AUX
-#define C3_AUX 2      // cache-policy bits of cvlr3_kernel's volume stores: nontemporal (0.769 -> 0.756 ms; 1: 0.762)
-#endif
-#ifndef C3_EARLY
-#define C3_EARLY 1    // the strip start waits for the own pixels only; the rows before the second barrier
-#endif
-#ifndef C3_SKIP
-#define C3_SKIP 0     // diagnostic builds only: 2 stores, 4 in-loop DMA, 8 dots
-#endif
+// cvlr3_kernel's volume stores are nontemporal (cache-policy bits 2; round 3: 0.769 -> 0.756 ms, 1: 0.762)
+constexpr int C3_AUX = 2;
 constexpr int C3_NX = 64;                                  // own pixels per strip
 constexpr int C3_RING = 64;                                // rows per parity sub-ring
 constexpr int C3_TS = 65;                                  // tile stride (floats per disparity)
@@ -381,12 +374,12 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
         const bool compute = q0 + 16 * wave < W;            // wave-uniform
         const int u = q0 + 16 * wave + 2 * p;
         // this strip's rows and own pixels have landed (every wave's DMA, hence the barrier); the
-        // previous strip's tile is complete.  C3_EARLY: only the own pixels are waited for here --
+        // previous strip's tile is complete.  Only the own pixels are waited for here --
         // per wave the ops after them are the previous strip's 32 emission stores (none before
         // strip 2) and this strip's 4-5 ring DMA instructions, and vmcnt retires in order -- so the
         // row block's DMA latency overlaps the own copy and the tile reads; the rows are waited for
         // before the second barrier.
-        if (!C3_EARLY || k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if (k == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if (WR) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
@@ -403,9 +396,9 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
             }
         }
         if (k > 0) emit_load();
-        if (C3_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this strip's rows
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this strip's rows
         cd_barrier();                                       // the own buffers and the tile are free
-        if (more && !(C3_SKIP & 4)) own_unit(q0 + C3_NX, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
+        if (more) own_unit(q0 + C3_NX, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
         {
             float *Tw = T + (e - dc) * C3_TS + 16 * wave + 2 * p;   // tile column of pixel u (u + 1: +1), disparity e
             const int obase = u + 1 - e;                    // odd: rows j even are odd, j odd even
@@ -413,7 +406,7 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
             const bool aok = u < W, bok = u + 1 < W;
             // wave-uniform (lanes past nd compute values that are never stored): no exec masking, so
             // the nine rows are one straight-line block the scheduler can pipeline across
-            if (compute && !(C3_SKIP & 8)) {
+            if (compute) {
                 // the 72 (row, 32-byte piece) steps with the pieces two steps ahead in flight
                 auto piece = [&](int jj, int mm, f32x4 &a, f32x4 &b) {
                     const int kj = (kb - (jj >> 1)) & (C3_RING - 1);
@@ -457,7 +450,7 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
                                          ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
                         Tw[(j - 1) * C3_TS] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
                     }
-                    if (k > 0 && !(C3_SKIP & 2)) emit_store(q0 - C3_NX, j);     // the previous strip's runs
+                    if (k > 0) emit_store(q0 - C3_NX, j);     // the previous strip's runs
                 }
             } else {
                 // past the row end: R's invalid fill only
@@ -465,13 +458,13 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
                 for (int j = 0; j < 8; j++) {
                     Tw[j * C3_TS] = invalid;
                     Tw[j * C3_TS + 1] = invalid;
-                    if (k > 0 && !(C3_SKIP & 2)) emit_store(q0 - C3_NX, j);
+                    if (k > 0) emit_store(q0 - C3_NX, j);
                 }
             }
         }
         // every wave's dots are done: the older row block's slots take the next strip's block
         cd_barrier();
-        if (more && !(C3_SKIP & 4)) ring_unit(q0 + C3_NX - dc, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
+        if (more) ring_unit(q0 + C3_NX - dc, wave & 1, (wave >> 1) ? 5 : 0, (wave >> 1) ? 9 : 5);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     cd_barrier();
