@@ -323,14 +323,6 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // read window k, the stagers write window k+1's four new tiles into the slots of the tiles
 // superstrip k-1 retired (ring = window + 4 tiles: 14 at D = 192, 112 KB).
 // ---------------------------------------------------------------------------
-#ifndef CV_PIPE
-#define CV_PIPE 1     // software-pipelined tile sweep in cv_wta_row2_kernel (0: the plain loop)
-#endif
-#ifndef CV_DIAG
-#define CV_DIAG 0     // timing-only builds (tools/cv_variants.py): 1 stagers skip the split + ring writes,
-                      // 8 and their loads; 2 compute waves skip the MFMAs + scores, 4 their ring reads,
-                      // 16 the left operand's split.  0 in the library.
-#endif
 constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
 constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
 
@@ -376,15 +368,8 @@ __device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *
     }
 }
 
-// SPLIT = 2 (A/B builds, -DCV_ROW_SPLIT=2): two compute waves per 32-pixel group, each sweeping half of the group's
-// right tiles (waves g and g + 4 sit on the same SIMD: two independent MFMA -> score chains per SIMD
-// where SPLIT = 1 has one), 8 compute + 4 stager waves = 768 threads.  The halves' (best, runner-up,
-// argmin, window norm, non-finite) partials meet through LDS after the superstrip's barrier and both
-// waves merge them the same way (fx_merge is symmetric: the maximum, its smallest index among equal
-// scores, and the second largest of the union -- exactly the SPLIT = 1 values), then each certifies
-// half of the group's pixels.
-template <bool WANT_MIN, int SPLIT>
-__global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
+template <bool WANT_MIN>
+__global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
                                                           int H, int W, int d0, int d1, int tlo0, int nw, int nt,
                                                           float *__restrict__ out_min, int32_t *__restrict__ out_arg,
                                                           float *__restrict__ out_disp, unsigned *__restrict__ counter,
@@ -394,13 +379,6 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
     uint4 *ring = rsm2;                                             // [nt][2 planes][32 px][8 chunks]
     unsigned *tmax = reinterpret_cast<unsigned *>(ring + nt * 512);  // [nt] max squared pixel norm (f32 bits)
     unsigned *tbad = tmax + nt;                                     // [nt] any non-finite channel
-    // SPLIT = 2: the halves' partials [parity of k][half][group][pixel]
-    float *pbest = reinterpret_cast<float *>(tbad + nt);
-    float *psec = pbest + 2 * SPLIT * 128;
-    int *parg = reinterpret_cast<int *>(psec + 2 * SPLIT * 128);
-    unsigned *pn2 = reinterpret_cast<unsigned *>(parg + 2 * SPLIT * 128);
-    unsigned *pwb = pn2 + 2 * SPLIT * 128;
-
     const int y = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -411,13 +389,12 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
     const int nss = (W + R2_NX - 1) / R2_NX;
     auto slot_of = [&](int T) { int r = T % nt; return r < 0 ? r + nt : r; };
 
-    if (wave >= 4 * SPLIT) {
+    if (wave >= 4) {
         // ---------------- stagers ----------------
-        const int sw = wave - 4 * SPLIT;
+        const int sw = wave - 4;
         // window 0 (nw tiles, tile tlo0 + t by wave t % 4) and this wave's tile of window 1
-        // (nw <= 14: at most 4 prologue tiles per stager; SPLIT = 2 loads them in two batches of two
-        // -- all four in flight at once would need 128 VGPRs, more than a 768-thread workgroup has)
-        constexpr int PB = SPLIT == 1 ? 4 : 2;         // tiles per batch
+        // (nw <= 14: at most 4 prologue tiles per stager, all in flight together)
+        constexpr int PB = 4;                          // tiles per batch
         float4 nv[8];
 #pragma unroll
         for (int b = 0; b < 4 / PB; b++) {
@@ -436,13 +413,8 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
             // then the load of window k+2's
             if (k + 1 < nss) {
                 const int T = tlo0 + R2_NEW * (k + 1) + nw - R2_NEW + sw;
-                if (CV_DIAG & 1) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) asm volatile("" ::"v"(nv[i].x), "v"(nv[i].y), "v"(nv[i].z), "v"(nv[i].w));
-                } else {
-                    r2_store(ring, tmax, tbad, slot_of(T), lane, nv);
-                }
-                if (k + 2 < nss && !(CV_DIAG & 8)) r2_load(frrow, W, T + R2_NEW, lane, nv);
+                r2_store(ring, tmax, tbad, slot_of(T), lane, nv);
+                if (k + 2 < nss) r2_load(frrow, W, T + R2_NEW, lane, nv);
             }
             __syncthreads();
         }
@@ -450,7 +422,7 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
     }
 
     // ---------------- compute waves ----------------
-    const int grp = wave & 3, hf = wave >> 2;       // pixel group, half of its right tiles
+    const int grp = wave & 3;                       // pixel group
     float4 lraw[8];
     auto load_left = [&](int kk) {
         const int xx = kk * R2_NX + RW_T * grp + j;
@@ -472,8 +444,6 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
         float nl = 0.0f;
         unsigned nmax2 = 0u, wbad = 0u;
         bool lbad = false;
-        const int pslot = ((k & 1) * SPLIT + hf) * 128 + 32 * grp + j;    // this wave's partial
-        const int oslot = ((k & 1) * SPLIT + (1 - hf)) * 128 + 32 * grp + j;   // the other half's
         if (xb < W) {          // wave-uniform
             rw_f16x8 bh[4], bl[4];
             float ssl = 0.0f;
@@ -484,8 +454,7 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     _Float16 hh, ll;
-                    if (CV_DIAG & 16) { hh = (_Float16)(float)e; ll = (_Float16)(float)s2; }
-                    else rw_split(v8[e], hh, ll);
+                    rw_split(v8[e], hh, ll);
                     bh[s2][e] = hh;
                     bl[s2][e] = ll;
                     ssl += v8[e] * v8[e];
@@ -503,24 +472,18 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
             for (int t = 0; t < 4; t++) { b1[t] = -__builtin_inff(); b2[t] = -__builtin_inff(); ag[t] = -1; }
             const int Ta = (xb - d1 + 1 + RW_T * 4096) / RW_T - 4096;
             const int Tb = (xb + 31 - d0 + RW_T * 4096) / RW_T - 4096;
-            int T0 = max(Ta, tlo), T1 = min(Tb, tlo + nw - 1);
-            if (SPLIT == 2) {                          // half 0: the first ceil(n / 2) tiles, half 1 the rest
-                const int mid = T0 + (T1 - T0 + 2) / 2;
-                if (hf == 0) T1 = mid - 1;
-                else T0 = mid;
-            }
+            const int T0 = max(Ta, tlo), T1 = min(Tb, tlo + nw - 1);
             int slot = slot_of(T0);
-#if CV_PIPE
-            if (CV_DIAG == 0) {
+            {
                 // software-pipelined sweep: tile i's 16 scores are interleaved with the 12 MFMAs of
                 // tile i + 1 (after two scores that cover the fragment reads' LDS latency: one MFMA,
                 // then the VALU of 1-2 scores, per gap -- the MFMA pipe runs while the scores issue).
                 // Same scores, same order of score updates: the same outputs.
                 // (every T in [T0, T1] is inside the band: Ta / Tb are its exact bounds)
                 const int n = T1 - T0 + 1;
-                // PD = 2 (CV_PIPE 2): tile i + 2's fragments are read during tile i's step, a whole
-                // step before its MFMAs (two fragment buffers); PD = 1: at the start of the step
-                constexpr int PD = CV_PIPE >= 2 ? 2 : 1;
+                // PD = 1: a tile's fragments are read at the start of the step before its MFMAs (PD = 2,
+                // a whole step earlier in two fragment buffers, spilled and measured slower, round 3)
+                constexpr int PD = 1;
                 rw_f16x8 fh[PD][4], fo[PD][4];
                 fx_floatx16 A[2];
                 auto nxt = [&](int sl2) { return sl2 + 1 == nt ? 0 : sl2 + 1; };
@@ -617,89 +580,6 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                         step(no{}, no{}, T0 + i2, sa, A[0], sa, A[1], fh[B1], fo[B1], sa, fh[0], fo[0]);
                     }
                 }
-            } else
-#endif
-            for (int T = T0; T <= T1; T++, slot = (slot + 1 == nt) ? 0 : slot + 1) {
-                const int dt = xb - RW_T * T;
-                const int dlo = dt - 31, dhi = dt + 31;
-                if (dhi < d0 || dlo >= d1) continue;     // wave-uniform
-                nmax2 = max(nmax2, tmax[slot]);
-                wbad |= tbad[slot];
-                const uint4 *tp = ring + slot * 512;
-                fx_floatx16 acc = {0};
-                rw_f16x8 ah[4], al[4];
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) {
-                    const int sl = fx_slot(j, 2 * s2 + h);
-                    if (CV_DIAG & 4) {
-                        ah[s2] = bh[s2] * (_Float16)(float)T;
-                        al[s2] = bl[s2];
-                    } else {
-                        ah[s2] = __builtin_bit_cast(rw_f16x8, tp[sl]);
-                        al[s2] = __builtin_bit_cast(rw_f16x8, tp[256 + sl]);
-                    }
-                }
-                if (CV_DIAG & 2) {
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; s2++) asm volatile("" ::"v"(ah[s2]), "v"(al[s2]));
-                    nmax2 += (unsigned)T;
-                    continue;
-                }
-                if (CV_DIAG & 128) {     // no MFMAs: scores from the fragments' bits (operands kept live)
-#pragma unroll
-                    for (int s2 = 0; s2 < 4; s2++)
-#pragma unroll
-                        for (int e = 0; e < 4; e++)
-                            acc[4 * s2 + e] = (float)ah[s2][2 * e] + (float)al[s2][2 * e + 1] + (float)bh[s2][e] +
-                                              (float)bl[s2][e + 4];
-                } else {
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) {
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2], bh[s2], acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bl[s2], acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bh[s2], acc, 0, 0, 0);
-                }
-                if (CV_DIAG & 64) {      // no scoring: the accumulators folded into one live value
-                    float z = 0.f;
-#pragma unroll
-                    for (int r = 0; r < 16; r++) asm volatile("" ::"v"(acc[r]));
-                    b1[0] = fmaxf(b1[0], acc[0] + (float)T);
-                    continue;
-                }
-                // register r holds d = dl - t - 8k (t = r & 3, k = r >> 2); chain t keeps d + t = dk[k]
-                // (four adds per tile instead of sixteen) and subtracts t once at the end
-                const int dl = dt + j - 4 * h;
-                int dk[4];
-#pragma unroll
-                for (int k2 = 0; k2 < 4; k2++) dk[k2] = dl - 8 * k2;
-                if (dlo >= d0 && dhi < d1) {
-                    // (an opaque statement: keeps this path a real scalar branch -- merged with the edge
-                    // path below into selects, every interior tile paid the edge path's 31 range
-                    // compares and 16 masking selects)
-                    asm volatile("");
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const int t = r & 3;
-                        const float sc = acc[r];
-                        const bool gt = sc > b1[t];
-                        if (!(CV_DIAG & 256)) ag[t] = gt ? dk[r >> 2] : ag[t];
-                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
-                        b1[t] = fmaxf(b1[t], sc);
-                    }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const int t = r & 3;
-                        const int d = dk[r >> 2] - t;
-                        const float sc = (d >= d0 && d < d1) ? acc[r] : -__builtin_inff();
-                        const bool gt = sc > b1[t];
-                        ag[t] = gt ? dk[r >> 2] : ag[t];
-                        b2[t] = __builtin_amdgcn_fmed3f(b1[t], b2[t], sc);
-                        b1[t] = fmaxf(b1[t], sc);
-                    }
-                }
             }
             // a chain that took a score holds d + t >= t >= 0; one that took none still holds -1
 #pragma unroll
@@ -712,22 +592,11 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                 const int aa = __shfl_xor(arg, 32, 64);
                 fx_merge(best, arg, second, bb, aa, ss2);
             }
-            if (SPLIT == 2 && h == 0) {
-                pbest[pslot] = best; psec[pslot] = second; parg[pslot] = arg;
-                pn2[pslot] = nmax2; pwb[pslot] = wbad;
-            }
         }
         // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
-        // barrier per superstrip orders both directions (and publishes the halves' partials, which
-        // alternate buffers by the parity of k: a half writes buffer k & 1 again only after the
-        // next barrier, which the other half passes after its read)
+        // barrier per superstrip orders both directions
         __syncthreads();
-        if (SPLIT == 2 && xb < W) {
-            fx_merge(best, arg, second, pbest[oslot], parg[oslot], psec[oslot]);
-            nmax2 = max(nmax2, pn2[oslot]);
-            wbad |= pwb[oslot];
-        }
-        if (xb < W && h == 0 && xok && (SPLIT == 1 || (j >> 4) == hf)) {
+        if (xb < W && h == 0 && xok) {
             const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
             const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
             const size_t p = rowpix + x;
@@ -742,7 +611,7 @@ __global__ __launch_bounds__(256 + 256 * SPLIT) void cv_wta_row2_kernel(const fl
                 if (out_arg) out_arg[p] = arg;
                 if (out_disp) out_disp[p] = (float)arg;
             } else {
-                if (!CV_DIAG) list[atomicAdd(counter, 1u)] = (int32_t)p;   // (diagnostic builds: no fix-ups)
+                list[atomicAdd(counter, 1u)] = (int32_t)p;
             }
         }
     }
@@ -767,23 +636,14 @@ static void row2_window(int d0, int d1, int &tlo0, int &nw)
     nw = fdiv(R2_NX - 1 - d0, RW_T) - tlo0 + 1;
 }
 
-#ifndef CV_ROW2
-#define CV_ROW2 1     // 0: the lock-step cv_wta_row_kernel (A/B builds)
-#endif
-#ifndef CV_ROW_SPLIT
-// compute waves per 32-pixel group of the warp-specialised kernel: 1, or 2 (measured no faster at
-// 1024^2 x 192: 0.255 vs 0.246 ms median, round-robin on one box -- the compute waves' MFMA -> score
-// chain is not what bounds the kernel)
-#define CV_ROW_SPLIT 1
-#endif
-// the halves' partials (5 words per pixel, two parities) after the ring and its per-tile words
-static size_t row2_smem(int nt) { return row_smem(nt) + (CV_ROW_SPLIT == 2 ? (size_t)5 * 2 * 2 * 128 * 4 : 0); }
+// the ring and its per-tile words
+static size_t row2_smem(int nt) { return row_smem(nt); }
 
 static bool row2_supported(int d0, int d1)
 {
     int tlo0 = 0, nw = 0;
     row2_window(d0, d1, tlo0, nw);
-    return CV_ROW2 && nw <= 14;           // prologue: <= 4 tiles per stager; ring <= 18 tiles
+    return nw <= 14;                      // prologue: <= 4 tiles per stager; ring <= 18 tiles
 }
 
 bool row_cert_supported(int d0, int d1)
@@ -797,16 +657,15 @@ void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int
                      float *out_disp, unsigned *counter, int32_t *list, hipStream_t st)
 {
     static std::atomic<uint64_t> attr{0};
-    constexpr int SPLIT = CV_ROW_SPLIT;
-    constexpr int NT2 = 256 + 256 * SPLIT;
+    constexpr int NT2 = 512;
     once_per_device(attr, [] {
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
         (void)hipFuncSetAttribute((const void *)cv_wta_row_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   150 * 1024);
-        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<true, SPLIT>,
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<false, SPLIT>,
+        (void)hipFuncSetAttribute((const void *)cv_wta_row2_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     });
     if (row2_supported(d0, d1)) {
@@ -814,10 +673,10 @@ void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int
         row2_window(d0, d1, tlo0, nw);
         const int nt = nw + R2_NEW;
         if (out_min)
-            cv_wta_row2_kernel<true, SPLIT><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
+            cv_wta_row2_kernel<true><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
                                                                           out_min, out_arg, out_disp, counter, list);
         else
-            cv_wta_row2_kernel<false, SPLIT><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
+            cv_wta_row2_kernel<false><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
                                                                            nullptr, out_arg, out_disp, counter, list);
         return;
     }

@@ -1,7 +1,7 @@
 """A/B timing of tools/_var/libsde_*.so (see build_file_variant.sh) against the in-tree library at
-1024^2 x 192: the GPU-path L/R volumes (sde_cost_volume HWD, L|R), one CBCA iteration of both
-sides (sde_cbca_pair), the 7-launch SGM pair (sde_sgm_8path_wta_pair).  Round-robin, median of 5;
-outputs checked bit-identical to the first library's."""
+1024^2 x 192: the GPU-path L/R volumes (sde_cost_volume HWD, L|R), sde_cbca_lr at 2 iterations
+(one volume aggregated + its shear), the 7-launch SGM pair (sde_sgm_8path_wta_pair).  Round-robin,
+median of 5; outputs checked bit-identical to the first library's."""
 import ctypes
 import glob
 import os
@@ -27,12 +27,13 @@ pen = [ops.sgm_penalties(i) for i in imgu8]
 disp = [torch.empty((H, W), device="cuda") for _ in range(2)]
 P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 here = os.path.dirname(os.path.abspath(__file__))
-sos = [_lib.LIB] + sorted(glob.glob(os.path.join(here, "_var", "libsde_*.so")))
+sos = [_lib.LIB] + sorted(f for f in glob.glob(os.path.join(here, "_var", "libsde_*.so"))
+                          if not os.path.basename(f).startswith("libsde_sgm_"))   # (sgm_variants.py's)
 libs = []
 for so in sos:
     lib = ctypes.CDLL(so)
     lib.sde_cost_volume.argtypes = [P, P, I, I, I, I, I, I, F, P, P, P]
-    lib.sde_cbca_pair.argtypes = [P, P, P, P, P, P, I, I, I, I, I, P]
+    lib.sde_cbca_lr.argtypes = [P, P, P, P, P, I, I, I, I, I, P, ctypes.c_size_t, P]
     lib.sde_sgm_8path_wta_pair.argtypes = [P] * 8 + [I, I, I, I, P]
     lib.sde_cv_wta.argtypes = [P, P, I, I, I, I, I, P, P, P, I, P, ctypes.c_int64, P]
     libs.append((os.path.basename(so), lib))
@@ -40,6 +41,7 @@ s = torch.cuda.current_stream().cuda_stream
 
 
 cvws = torch.empty(_lib.lib.sde_cv_wta_workspace_bytes(H, W), dtype=torch.uint8, device="cuda")
+cbws = torch.empty(ops.cbca_workspace_bytes(H, W), dtype=torch.uint8, device="cuda")
 
 
 def run(lib, w):
@@ -50,8 +52,8 @@ def run(lib, w):
         assert lib.sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
                                    vol[1].data_ptr(), s) == 0
     elif w == "cbca":
-        assert lib.sde_cbca_pair(vol[0].data_ptr(), vol[2].data_ptr(), vol[1].data_ptr(), vol[3].data_ptr(),
-                                 arms[0].data_ptr(), arms[1].data_ptr(), H, W, D, 14, 1, s) == 0
+        assert lib.sde_cbca_lr(vol[0].data_ptr(), vol[1].data_ptr(), vol[2].data_ptr(), arms[0].data_ptr(),
+                               arms[1].data_ptr(), H, W, D, 14, 2, cbws.data_ptr(), cbws.numel(), s) == 0
     else:
         assert lib.sde_sgm_8path_wta_pair(vol[0].data_ptr(), pen[0].data_ptr(), vol[2].data_ptr(), disp[0].data_ptr(),
                                           vol[1].data_ptr(), pen[1].data_ptr(), vol[3].data_ptr(), disp[1].data_ptr(),
