@@ -349,7 +349,11 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     double P = 0.0;
     uint32_t N = 0;
     sP[(RS - 1) * 64 + lane] = 0.0;               // Q(fs - 1) = 0, N(fs - 1) = 0
-    sN[(RS - 1) * 64 + lane] = 0;
+    // count ring: lane l's u16 sits at (l % 32) * 2 + l / 32 of its slot row, so a 32-lane half
+    // touches 32 different dwords of one row -- distinct banks whatever slot each lane reads (the
+    // straight [slot][lane] layout put lanes 2k and 2k+1 in one bank: 2-way conflicts)
+    const int ln = ((lane & 31) << 1) | (lane >> 5);
+    sN[(RS - 1) * 64 + ln] = 0;
 
     // step j of a block at front f; loads address rows relative to fbase, stores relative to fb - R - 1
     // PRE: the walk's first block (its first fc - fs <= 3 positions precede the chain)
@@ -363,7 +367,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         const int vu = sy & 0xFFFF, vd = sy >> 16;
         const uint32_t ib = ring_slot<RS>(j - R - 1 + vd), ia = ring_slot<RS>(j - R - 2 - vu);
         const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
-        const uint16_t nb = sN[ib * 64 + lane], na = sN[ia * 64 + lane];
+        const uint16_t nb = sN[ib * 64 + ln], na = sN[ia * 64 + ln];
         __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front f: chain (rows >= fc), count contribution and vertical support
         const uint32_t a = ruint(Ab, j);
@@ -379,7 +383,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         P += on ? (double)cr[slot] : 0.0;
         N += on ? ((m02 + m13) & 0xFFFFu) + 1u : 0u;
         sP[j * 64 + lane] = P;
-        sN[j * 64 + lane] = (uint16_t)N;
+        sN[j * 64 + ln] = (uint16_t)N;
         sup[j % U] = (m02 >> 16) | (m13 & 0xFFFF0000u);
         if (j % 4 == 3) Bq[j / 4] = arm_q(f + RS - 3);      // the next block's rows f + RS - 3 ..
         const uint32_t so = clamp ? rowv * (uint32_t)(min(f + PF, H - 1) - fbase) : sld;
