@@ -324,8 +324,9 @@ int sde_cbca_arms(const float *img, int64_t pitch, int H, int W, int L1, float t
  */
 #define SDE_CBCA_SEG 256
 
-/* Workspace of the aggregation entry points (column-major copies of both
- * images' arms): 8 * W * roundup(H, 4) bytes. */
+/* Workspace of the aggregation entry points (a column-major copy of the left
+ * image's arms for the vertical pass): 4 * W * roundup(H, 4) bytes (ABI 3 asked
+ * for 8 *: larger buffers stay valid). */
 size_t sde_cbca_workspace_bytes(int H, int W);
 
 /*

@@ -129,7 +129,7 @@ struct CbcaArgs {
     const float *src;
     float *dst;
     const uint32_t *al, *ar;       // row-major arms (left / right image): horizontal pass
-    const uint32_t *alT, *arT;     // column-major arms (pitch Hp): vertical pass
+    const uint32_t *alT;           // column-major left-image arms (pitch Hp): vertical pass
     int H, W, D, M, Hp;
     int nseg, ndc;
     int64_t nitems;
@@ -303,8 +303,8 @@ template <int R>
 __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, double *__restrict__ sP,
                                             uint16_t *__restrict__ sN, const double *__restrict__ tab)
 {
-    constexpr int RS = 2 * R + 2, PF = RS, U = R + 1, NQ = RS / 4;
-    static_assert(RS % 4 == 0 && RS % U == 0, "ring sizes");
+    constexpr int RS = 2 * R + 2, PF = RS, U = R + 1;
+    static_assert(RS % U == 0, "ring sizes");
     const int lane = threadIdx.x & 63;
     const int H = A.H, W = A.W, D = A.D, M = A.M, Hp = A.Hp;
     const int d0 = 64 * c, d = d0 + lane;
@@ -319,24 +319,27 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     // ranges covering the rows a block touches (< 2^31 bytes: the shape check)
     const uint32_t win = (uint32_t)(RS + PF + R + 1) * rowv;
     const __amdgpu_buffer_rsrc_t ra = cb_rsrc(A.alT + (size_t)x * Hp, 4u * (uint32_t)Hp);
-    const __amdgpu_buffer_rsrc_t rb = cb_rsrc(A.arT, 4u * (uint32_t)W * (uint32_t)Hp);
-    const uint32_t bcol = lane_ok ? 4u * (uint32_t)(x - d) * (uint32_t)Hp : CB_OOB;
+    // right-image arms from the ROW-major copy: at a row, lane d reads column x - d, so the wave's
+    // 64 lanes read 64 adjacent words (one 256-B run) -- the column-major copy made every dwordx4
+    // a gather of 64 cache lines
+    const __amdgpu_buffer_rsrc_t rb = cb_rsrc(A.ar, 4u * (uint32_t)W * (uint32_t)H);
+    const uint32_t bcol = lane_ok ? 4u * (uint32_t)(x - d) : CB_OOB;
 
     float cr[PF];
-    u32x4 Bq[NQ];                // right-image arms of rows fb + 4m .. +3 (per lane); Bq[m] is
-                                 // reloaded with the next block's rows once its last row is used
+    uint32_t Bq[RS];             // right-image arm of row fb + j (per lane); slot j is reloaded with
+                                 // the next block's row once step j has used it
     uint32_t A0, A1;             // left-image arm of row fb + lane (lanes < RS), pairs by block parity
     uint32_t sup[U];             // (vu | vd << 16) of the last U front positions
-    auto arm_q = [&](int row) {  // rows row .. row + 3 of the right image at x - d
-        const uint32_t off = bcol == CB_OOB ? CB_OOB : bcol + 4u * (uint32_t)row;
-        return __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0);
+    auto arm_r = [&](int row) {  // row `row` of the right image at x - d (rows past H read 0)
+        const uint32_t off = bcol == CB_OOB ? CB_OOB : bcol + 4u * (uint32_t)W * (uint32_t)row;
+        return __builtin_amdgcn_raw_buffer_load_b32(rb, off, 0, 0);
     };
     // the arms first: loop-carried registers loaded after the cost prefetch would make the entry
     // path's waits for them (merged into every block start) drain the whole prefetch
     A0 = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + lane), 0, 0);
     A1 = __builtin_amdgcn_raw_buffer_load_b32(ra, 4u * (uint32_t)(fs + RS + lane), 0, 0);
 #pragma unroll
-    for (int m = 0; m < NQ; m++) Bq[m] = arm_q(fs + 4 * m);
+    for (int m = 0; m < RS; m++) Bq[m] = arm_r(fs + m);
     {
         const __amdgpu_buffer_rsrc_t rc0 = cb_rsrc(A.src + ((size_t)fs * W + x) * D, win);
 #pragma unroll
@@ -364,14 +367,23 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         // overwrites it below), its prefix / count reads before the front's writes
         const int t = f - R - 1;
         const uint32_t sy = sup[j % U];
-        const int vu = sy & 0xFFFF, vd = sy >> 16;
+        // the halves unpacked by opaque instructions: folded into SDWA adds, every step's slot
+        // constant became a VGPR held across the loop (~70 registers)
+        // (R = 31 keeps the plain form: with the asm its SGPR pressure forces an illegal VGPR-to-SGPR
+        // copy in the compiler)
+        uint32_t vu_u = sy & 0xFFFFu, vd_u = sy >> 16;
+        if (R <= 15) {
+            asm("v_and_b32 %0, 0xffff, %1" : "=v"(vu_u) : "v"(sy));
+            asm("v_lshrrev_b32 %0, 16, %1" : "=v"(vd_u) : "v"(sy));
+        }
+        const int vu = (int)vu_u, vd = (int)vd_u;
         const uint32_t ib = ring_slot<RS>(j - R - 1 + vd), ia = ring_slot<RS>(j - R - 2 - vu);
         const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
         const uint16_t nb = sN[ib * 64 + ln], na = sN[ia * 64 + ln];
         __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front f: chain (rows >= fc), count contribution and vertical support
         const uint32_t a = ruint(Ab, j);
-        const uint32_t bw = Bq[j / 4][j % 4];
+        const uint32_t bw = Bq[j];
         const uint32_t a02 = a & 0x00FF00FFu, a13 = (a >> 8) & 0x00FF00FFu;
         const uint32_t b02 = bw & 0x00FF00FFu, b13 = (bw >> 8) & 0x00FF00FFu;
         // per 16-bit half: (min l, min u) and (min r, min d)
@@ -385,7 +397,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         sP[j * 64 + lane] = P;
         sN[j * 64 + ln] = (uint16_t)N;
         sup[j % U] = (m02 >> 16) | (m13 & 0xFFFF0000u);
-        if (j % 4 == 3) Bq[j / 4] = arm_q(f + RS - 3);      // the next block's rows f + RS - 3 ..
+        Bq[j] = arm_r(f + RS);                              // the next block's row
         const uint32_t so = clamp ? rowv * (uint32_t)(min(f + PF, H - 1) - fbase) : sld;
         cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
         sld = opq_s(sld + rowv);
@@ -566,7 +578,7 @@ __global__ void cbca_recip_kernel(double *out, int n)
 // ---------------------------------------------------------------------------------------------
 static inline int cb_hp(int H) { return (H + 3) & ~3; }
 
-static size_t cbca_ws_bytes(int H, int W) { return 2 * sizeof(uint32_t) * (size_t)cb_hp(H) * (size_t)W; }
+static size_t cbca_ws_bytes(int H, int W) { return sizeof(uint32_t) * (size_t)cb_hp(H) * (size_t)W; }
 
 // Resident workgroups of a pass kernel (occupancy x CUs), per device and kernel.
 template <typename K>
@@ -590,10 +602,10 @@ static int cb_grid(int64_t nitems, int resident)
 // One left-coordinate volume: iters x (horizontal src -> tmp, vertical tmp -> src), in place.
 template <int R>
 static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uint32_t *ar, const uint32_t *alT,
-                            const uint32_t *arT, int H, int W, int D, int L1, int iters, hipStream_t st)
+                            int H, int W, int D, int L1, int iters, hipStream_t st)
 {
     CbcaArgs h{};
-    h.al = al, h.ar = ar, h.alT = alT, h.arT = arT;
+    h.al = al, h.ar = ar, h.alT = alT;
     h.H = H, h.W = W, h.D = D, h.M = L1 - 1, h.Hp = cb_hp(H);
     h.ndc = (D + 63) / 64;
     CbcaArgs v = h;
@@ -642,14 +654,13 @@ static int cbca_left(float *cv, float *tmp, const uint32_t *al, const uint32_t *
 {
     if (iters == 0) return SDE_OK;
     const int Hp = cb_hp(H);
-    uint32_t *alT = (uint32_t *)ws, *arT = alT + (size_t)Hp * W;
+    uint32_t *alT = (uint32_t *)ws;
     const dim3 tg((W + 31) / 32, (Hp + 31) / 32);
     cbca_transpose_kernel<<<tg, 256, 0, st>>>(al, alT, H, W, Hp);
-    cbca_transpose_kernel<<<tg, 256, 0, st>>>(ar, arT, H, W, Hp);
     switch (cbca_r(L1)) {
-    case 13: cbca_left_iters<13>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
-    case 15: cbca_left_iters<15>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
-    default: cbca_left_iters<31>(cv, tmp, al, ar, alT, arT, H, W, D, L1, iters, st); break;
+    case 13: cbca_left_iters<13>(cv, tmp, al, ar, alT, H, W, D, L1, iters, st); break;
+    case 15: cbca_left_iters<15>(cv, tmp, al, ar, alT, H, W, D, L1, iters, st); break;
+    default: cbca_left_iters<31>(cv, tmp, al, ar, alT, H, W, D, L1, iters, st); break;
     }
     return launch_status();
 }

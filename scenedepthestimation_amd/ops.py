@@ -510,7 +510,7 @@ def cbca_arms(img, L1=14, tau=0.02, out=None):
 
 
 def cbca_workspace_bytes(H, W):
-    """Bytes of the aggregation workspace (column-major arms of both images, sde_cbca_workspace_bytes)."""
+    """Bytes of the aggregation workspace (column-major left-image arms, sde_cbca_workspace_bytes)."""
     return int(lib.sde_cbca_workspace_bytes(int(H), int(W)))
 
 

@@ -139,7 +139,7 @@ def test_argument_validation_without_gpu():
     assert lib.sde_preprocess_scratch_bytes(1024, 1024) == 768 and lib.sde_preprocess_scratch_bytes(3, 5) == 256
     assert lib.sde_tower_packed_floats(0, 64) == -1
     W8 = lib.sde_cbca_workspace_bytes(4, 8)
-    assert W8 == 8 * 8 * 4 and lib.sde_cbca_workspace_bytes(5, 7) == 8 * 7 * 8 and lib.sde_cbca_workspace_bytes(0, 7) == 0
+    assert W8 == 4 * 8 * 4 and lib.sde_cbca_workspace_bytes(5, 7) == 4 * 7 * 8 and lib.sde_cbca_workspace_bytes(0, 7) == 0
     assert lib.sde_cbca_pair(1, 2, 3, 1, 5, 6, 4, 8, 8, 14, 1, 7, W8, N) == ERR                   # aliased buffers
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 8, 8, 33, 1, 7, W8, N) == ERR                   # L1 > 32
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 4, 8, 8, 14, 1, 7, W8 - 1, N) == ERR               # workspace
