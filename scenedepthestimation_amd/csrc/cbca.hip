@@ -500,10 +500,12 @@ __global__ __launch_bounds__(64 * CbV<R>::WPB, 2) void cbca_v_kernel(const CbcaA
 // workgroups per CU, and each wave keeps its 16 loads of a batch in flight together.
 // ---------------------------------------------------------------------------------------------
 constexpr int RT_NP = 64, RT_ND = 64;
+// S: the rotation's sign; WIDE: W >= 64 (a batch's pieces wrap the row at most once)
+template <int S, bool WIDE>
 __global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restrict__ in, float *__restrict__ out, int H,
-                                                          int W, int D, int s, int valid_only, int64_t ntiles)
+                                                          int W, int D, int valid_only, int64_t ntiles)
 {
-    __shared__ float rbuf[RT_NP * RT_ND];
+    __shared__ float rbuf[RT_NP * RT_ND + 64];   // + dump words for the lanes past a piece's run
     const int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;
     const int nxs = (W + RT_NP - 1) / RT_NP, nds = (D + RT_ND - 1) / RT_ND;
@@ -511,41 +513,48 @@ __global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restric
     const int rem = (int)(tile - (int64_t)y * nxs * nds);
     const int x0 = (rem / nds) * RT_NP, d0 = (rem % nds) * RT_ND;
     const int nd = min(RT_ND, D - d0);
-    // wave-uniform by construction; readfirstlane lets the piece indices live in SGPRs
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t rowbytes = 4u * (uint32_t)W * (uint32_t)D;
     const __amdgpu_buffer_rsrc_t ri = cb_rsrc(in + (size_t)y * W * D, rowbytes);
     const __amdgpu_buffer_rsrc_t ro = cb_rsrc(out + (size_t)y * W * D, rowbytes);
     // piece r (0 <= r < RT_NP + nd - 1): source pixel (x0 + base + r) mod W; output pixel p of relative
-    // disparity e = d - d0 is p = r - e (s > 0) or p = r + e - (nd - 1) (s < 0)
-    const int base = s > 0 ? d0 : -d0 - (nd - 1);
+    // disparity e = d - d0 is p = r - e (S > 0) or p = r + e - (nd - 1) (S < 0)
+    const int base = S > 0 ? d0 : -d0 - (nd - 1);
     const int np = RT_NP + nd - 1;
     constexpr int RB = 16;        // pieces per wave in flight: a batch's loads all issue before its LDS writes
     for (int r0 = wave; r0 < np; r0 += 4 * RB) {
         float v[RB];
         int at[RB];
-        // source pixel of piece r0 in [0, W) (one modulo per batch; the batch's pieces step by 4)
+        // source pixel of piece r0 in [0, W): one modulo per batch (scalar)
         int q0 = (x0 + base + r0) % W;
         if (q0 < 0) q0 += W;
+        // the per-piece bookkeeping on the vector ALUs: as scalar code (one scalar unit per CU for
+        // four SIMDs) it bound the kernel -- PMC 2.3e8 SALU instructions per launch
+        int rv = r0, qv = q0;
+        asm volatile("" : "+v"(rv), "+v"(qv));
 #pragma unroll
         for (int b = 0; b < RB; b++) {
-            const int r = r0 + 4 * b;
-            const int elo = s > 0 ? max(0, r - (RT_NP - 1)) : max(0, nd - 1 - r);
-            const int ehi = s > 0 ? min(nd - 1, r) : min(nd - 1, nd - 1 - r + RT_NP - 1);
+            const int r = rv + 4 * b;
+            const int elo = S > 0 ? max(0, r - (RT_NP - 1)) : max(0, nd - 1 - r);
+            const int ehi = S > 0 ? min(nd - 1, r) : min(nd - 1, nd - 1 - r + RT_NP - 1);
             const int e = elo + lane, d = d0 + e;
-            const int p = s > 0 ? r - e : r + e - (nd - 1);
+            const int p = S > 0 ? r - e : r + e - (nd - 1);
             const int x = x0 + p;
-            int q = q0 + 4 * b;
-            while (q >= W) q -= W;                // (uniform; one compare unless W < 4 * RB)
-            const bool inr = r < np && e <= ehi;
-            const bool ok = inr && x < W && (!valid_only || x + d < W);
+            int q = qv + 4 * b;
+            if (WIDE) q = q >= W ? q - W : q;
+            else q %= W;
+            // the conditions as one signed minimum each (vector ops, no scalar mask algebra); the
+            // offset computed before the select (not sunk into an exec-masked branch)
+            const int in_m = min(ehi - e, np - 1 - r);                           // >= 0: inside the run
+            const int ok_m = min(in_m, min(W - 1 - x, valid_only ? W - 1 - x - d : 0));
+            uint32_t vraw = 4u * ((uint32_t)q * D + d);
+            asm volatile("" : "+v"(vraw));
             v[b] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 ri, ok ? 4u * ((uint32_t)q * D + d) : CB_OOB, 0, CBCA_NT & 1 ? 2 : 0));
-            at[b] = inr ? p * RT_ND + e : -1;
+                                                 ri, ok_m >= 0 ? vraw : CB_OOB, 0, CBCA_NT & 1 ? 2 : 0));
+            at[b] = in_m >= 0 ? p * RT_ND + e : RT_NP * RT_ND + lane;
         }
 #pragma unroll
-        for (int b = 0; b < RB; b++)
-            if (at[b] >= 0) rbuf[at[b]] = v[b];
+        for (int b = 0; b < RB; b++) rbuf[at[b]] = v[b];
     }
     __syncthreads();
     // output pixels x0 + p (wave w: pixels w, w + 4, ...), one run of nd floats each, WB per batch
@@ -558,7 +567,7 @@ __global__ __launch_bounds__(256) void cbca_rotate_kernel(const float *__restric
         for (int b = 0; b < WB; b++) {
             const int p = i0 + 4 * b + wave, x = x0 + p, d = d0 + lane;
             const bool inr = x < W && lane < nd;
-            v[b] = inr ? rbuf[p * RT_ND + lane] : 0.0f;
+            v[b] = rbuf[p * RT_ND + lane];
             vo[b] = inr && (!valid_only || x + d < W) ? 4u * ((uint32_t)x * D + d) : CB_OOB;
         }
 #pragma unroll
@@ -633,7 +642,14 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
 static void cbca_rotate(const float *in, float *out, int H, int W, int D, int s, bool valid_only, hipStream_t st)
 {
     const int64_t ntiles = (int64_t)H * ((W + RT_NP - 1) / RT_NP) * ((D + RT_ND - 1) / RT_ND);
-    cbca_rotate_kernel<<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, s, valid_only ? 1 : 0, ntiles);
+    const int vo = valid_only ? 1 : 0;
+    if (s > 0) {
+        if (W >= 64) cbca_rotate_kernel<1, true><<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, vo, ntiles);
+        else cbca_rotate_kernel<1, false><<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, vo, ntiles);
+    } else {
+        if (W >= 64) cbca_rotate_kernel<-1, true><<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, vo, ntiles);
+        else cbca_rotate_kernel<-1, false><<<(unsigned)ntiles, 256, 0, st>>>(in, out, H, W, D, vo, ntiles);
+    }
 }
 
 // Shapes the 32-bit offsets cover (refused with SDE_ERR_ARG otherwise): a row of the volume and a
