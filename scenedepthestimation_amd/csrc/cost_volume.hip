@@ -440,15 +440,29 @@ __global__ __launch_bounds__(256, 2) void cvlr3_kernel(const float *__restrict__
                             }
                         }
                     }
-                    if (j <= 7) {
-                        const float sm = ((xb[0].x + xb[0].y) + (xb[1].x + xb[1].y)) +
-                                         ((xb[2].x + xb[2].y) + (xb[3].x + xb[3].y));
-                        Tw[j * C3_TS + 1] = (bok && o >= 0) ? -(0.0f + sm) : invalid;
-                    }
-                    if (j >= 1) {
-                        const float sm = ((xa[0].x + xa[0].y) + (xa[1].x + xa[1].y)) +
-                                         ((xa[2].x + xa[2].y) + (xa[3].x + xa[3].y));
-                        Tw[(j - 1) * C3_TS] = (aok && o >= 0) ? -(0.0f + sm) : invalid;
+                    // the pairwise tree ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)): the first level within
+                    // each pixel's channel pairs as single adds, the rest packed across the two pixels
+                    // (left to itself, the compiler packed the first level with three moves per add)
+                    if (j >= 1 && j <= 7) {
+                        f32x2 s[4];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            float ua, ub;
+                            asm("v_add_f32 %0, %1, %2" : "=v"(ua) : "v"(xa[t].x), "v"(xa[t].y));
+                            asm("v_add_f32 %0, %1, %2" : "=v"(ub) : "v"(xb[t].x), "v"(xb[t].y));
+                            s[t] = f32x2{ua, ub};
+                        }
+                        const f32x2 sm = f32x2{0.0f, 0.0f} + ((s[0] + s[1]) + (s[2] + s[3]));
+                        Tw[j * C3_TS + 1] = (bok && o >= 0) ? -sm.y : invalid;
+                        Tw[(j - 1) * C3_TS] = (aok && o >= 0) ? -sm.x : invalid;
+                    } else {
+                        const f32x2 *x = j == 0 ? xb : xa;
+                        float u[4];
+#pragma unroll
+                        for (int t = 0; t < 4; t++) asm("v_add_f32 %0, %1, %2" : "=v"(u[t]) : "v"(x[t].x), "v"(x[t].y));
+                        const float sm = 0.0f + ((u[0] + u[1]) + (u[2] + u[3]));
+                        if (j == 0) Tw[1] = (bok && o >= 0) ? -sm : invalid;
+                        else Tw[7 * C3_TS] = (aok && o >= 0) ? -sm : invalid;
                     }
                     if (k > 0) emit_store(q0 - C3_NX, j);     // the previous strip's runs
                 }

@@ -1,5 +1,5 @@
 """A/B timing of tools/_var/libsde_*.so (see build_file_variant.sh) against the in-tree library at
-1024^2 x 192: the GPU-path L/R volumes (sde_cost_volume HWD, L|R), sde_cbca_lr at 2 iterations
+1024^2 x 192: the GPU-path L/R volumes (sde_cost_volume HWD, L|R; cvlrl: L only), sde_cbca_lr at 2 iterations
 (one volume aggregated + its shear), the 7-launch SGM pair (sde_sgm_8path_wta_pair).  Round-robin,
 median of 5; outputs checked bit-identical to the first library's."""
 import ctypes
@@ -51,6 +51,9 @@ def run(lib, w):
     elif w == "cvlr":
         assert lib.sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 3, 1.0, vol[0].data_ptr(),
                                    vol[1].data_ptr(), s) == 0
+    elif w == "cvlrl":   # the aggregation path's sweep: the left volume only
+        assert lib.sde_cost_volume(fl.data_ptr(), fr.data_ptr(), H, W, 64, D, 1, 1, 1.0, vol[0].data_ptr(),
+                                   None, s) == 0
     elif w == "cbca":
         assert lib.sde_cbca_lr(vol[0].data_ptr(), vol[1].data_ptr(), vol[2].data_ptr(), arms[0].data_ptr(),
                                arms[1].data_ptr(), H, W, D, 14, 2, cbws.data_ptr(), cbws.numel(), s) == 0
@@ -62,7 +65,8 @@ def run(lib, w):
 
 def outputs(w):
     torch.cuda.synchronize()
-    return [t.clone() for t in (vol[:2] if w not in ("sgm", "cvwta") else disp[:1] if w == "cvwta" else disp)]
+    return [t.clone() for t in (vol[:1] if w == "cvlrl" else vol[:2] if w not in ("sgm", "cvwta") else
+                                disp[:1] if w == "cvwta" else disp)]
 
 
 for w in what:
