@@ -168,6 +168,11 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <int N>
+struct SgmV {
+    typedef float T __attribute__((ext_vector_type(N)));
+};
+
 template <int DPL>
 __device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL])
 {
@@ -181,6 +186,14 @@ __device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL])
 // operands only)
 template <int DPL>
 __device__ __forceinline__ bool any_nonfinite(const float (&c)[DPL], float p1, float p2)
+{
+    bool nf = __builtin_amdgcn_classf(p1, 0x207) | __builtin_amdgcn_classf(p2, 0x207);
+#pragma unroll
+    for (int i = 0; i < DPL; i++) nf |= __builtin_amdgcn_classf(c[i], 0x207);
+    return __builtin_amdgcn_ballot_w64(nf) != 0;
+}
+template <int DPL>
+__device__ __forceinline__ bool any_nonfinite_v(const typename SgmV<DPL>::T &c, float p1, float p2)
 {
     bool nf = __builtin_amdgcn_classf(p1, 0x207) | __builtin_amdgcn_classf(p2, 0x207);
 #pragma unroll
@@ -377,10 +390,17 @@ __device__ __forceinline__ void wta_block_store(float bv, int ba, int px, int q,
     if (q == 0 && px >= 0) disp[px] = (float)(ba == 0x7fffffff ? 0 : ba);
 }
 
+// the destination of the S stores a step must not make (sgm_scan_kernel): one row of the widest lane
+// block, rewritten by every wave that needs it, never read
+__device__ float sgm_dump[64 * 16];
+
+// a slot's DPL costs / S values as ONE vector value: as separate floats, the loop-header phis of
+// the elements did not coalesce with the dwordx{DPL} load's register tuple, and the loop latch
+// copied them back -- waiting for each slot's load, i.e. draining the prefetch ring
 template <int DPL>
 struct Slot {
-    float c[DPL];
-    float s[DPL];
+    typename SgmV<DPL>::T c;
+    typename SgmV<DPL>::T s;
     float p1, p2;   // p1 as loaded: the step applies `pin` (a select at issue would wait for the load);
                     // SGM_WALK: this pixel's P1 channel, the NEXT step's P1
     size_t off;     // voxel offset of (r, c, d = 0)
@@ -607,6 +627,10 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
         ahead.advance(g);
     }
+    // the ring has landed before the loop: otherwise the loop header merges this entry path (the
+    // fill's loads in another order, fewer ops after each) with the latch, and the waitcnt pass sizes
+    // the first steps' waits for the entry path -- vmcnt(1..3) every PF steps, a drained ring
+    __builtin_amdgcn_s_waitcnt(0xF70);          // vmcnt(0)
 
     double L[DPL];
     double m = 1.0, mP2 = 1.0;
@@ -627,11 +651,17 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
         for (int j = 0; j < PF; j++) {
             const int k = k0 + j;     // steps k >= n compute on a clamped pixel and store nothing
             const Slot<DPL> &sl = ring[j];
-            const float p1f = SGM_WALK ? (sl.restart ? 0.0f : p1c) : (sl.pin ? sl.p1 : 0.0f), p2f = sl.p2;
-            if (SGM_WALK) p1c = sl.p1;      // read before the slot's refill at the end of this step
+            const float p1f = SGM_WALK ? (sl.restart ? 0.0f : p1c) : (sl.pin ? sl.p1 : 0.0f);
+            // (wave-uniform; into an SGPR for the reason given for p1c below)
+            const float p2f = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sl.p2)));
+            // read before the slot's refill at the end of this step, into an SGPR: carried as the
+            // slot's own VGPR it stayed live across the refill, so the refill took other registers and
+            // the loop latch copied every slot's penalty pair back -- waiting for each load in turn,
+            // which drained the prefetch ring once per PF steps
+            if (SGM_WALK) p1c = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sl.p1)));
             if (DU) {
-                if (FIRST && !redo) redo = any_nonfinite<DPL>(sl.c, p1f, p2f);
-            } else if (kf < 0 && k < g.n && any_nonfinite<DPL>(sl.c, p1f, p2f)) {
+                if (FIRST && !redo) redo = any_nonfinite_v<DPL>(sl.c, p1f, p2f);
+            } else if (kf < 0 && k < g.n && any_nonfinite_v<DPL>(sl.c, p1f, p2f)) {
                 // every state so far is finite; from step k on the line is redone in the reference's
                 // exact arithmetic after this loop, which stores nothing more for it
                 kf = k;
@@ -725,21 +755,26 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     else wta_merge(mv_b, mv_a, v2, a2);
                     if (j == PF - 1) wta_block_store<G>(mv_b, mv_a, wpx[(buf ^ 1) * PF + wst], wq, sd.disp);
                 }
-            } else if (k < g.n && keep && !(SGM_DIAG & 2)) {
-                if (VEC) {
-                    if (dbase < D) {
-                        FVec<DPL> ov;
+            } else if (VEC && !(SGM_DIAG & 2)) {
+                // every step stores: a step that must not (past the line's end, a line gone faithful)
+                // writes the dump row instead.  A store behind a branch left the waitcnt pass unsure
+                // how many stores were in flight, so it waited for loads issued 2-3 steps back
+                // instead of PF: the prefetch ring was mostly idle.
+                float *const sbase = (k < g.n && keep) ? sd.S + sl.off : sgm_dump;
+                if (dbase < D) {
+                    FVec<DPL> ov;
 #pragma unroll
-                        for (int i = 0; i < DPL; i++) ov.v[i] = o[i];
-                        if (SGM_NT & 2) {
+                    for (int i = 0; i < DPL; i++) ov.v[i] = o[i];
+                    if (SGM_NT & 2) {
 #pragma unroll
-                            for (int i = 0; i < DPL; i++)
-                                __builtin_nontemporal_store(o[i], sd.S + sl.off + (unsigned)dbase + i);
-                        } else {
-                            *reinterpret_cast<FVec<DPL> *>(sd.S + sl.off + dbase) = ov;
-                        }
+                        for (int i = 0; i < DPL; i++)
+                            __builtin_nontemporal_store(o[i], sbase + (unsigned)dbase + i);
+                    } else {
+                        *reinterpret_cast<FVec<DPL> *>(sbase + dbase) = ov;
                     }
-                } else {
+                }
+            } else if (k < g.n && keep && !(SGM_DIAG & 2)) {
+                {
 #pragma unroll
                     for (int i = 0; i < DPL; i++)
                         if (dbase + i < D) sd.S[sl.off + dbase + i] = o[i];
