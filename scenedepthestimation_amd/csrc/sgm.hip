@@ -629,8 +629,11 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     }
     // the ring has landed before the loop: otherwise the loop header merges this entry path (the
     // fill's loads in another order, fewer ops after each) with the latch, and the waitcnt pass sizes
-    // the first steps' waits for the entry path -- vmcnt(1..3) every PF steps, a drained ring
-    __builtin_amdgcn_s_waitcnt(0xF70);          // vmcnt(0)
+    // the first steps' waits for the entry path -- vmcnt(1..3) every PF steps, a drained ring.
+    // Except in the first pass (cost loads, S stores, no S loads): there the drained ring is the
+    // faster one, 619 against 646 us per launch (profiles/r04/sgm_ab_ring_waits.txt; PF 4 or 6:
+    // 634 / 647 us) -- the other six launches gain from the full ring (DU-RL + WTA 670 -> 620 us)
+    if (!(FIRST && DU)) __builtin_amdgcn_s_waitcnt(0xF70);          // vmcnt(0)
 
     double L[DPL];
     double m = 1.0, mP2 = 1.0;
