@@ -27,16 +27,10 @@
 // right image sides (the reference's k loop) run in the same launch (grid.y).
 #include "sde_common.h"
 
-#ifndef SGM_DIAG
-#define SGM_DIAG 0    // profiling builds only (tools/build_sgm_variant.sh): 1 loads from a hot 64-pixel region, 2 no S stores
-#endif
 // The cost and S streams are touched once per pass: nontemporal loads and stores (1 | 2).  Both
 // together: 6.44 -> 5.96 ms for the 7-launch pair (either alone: no change; tools/sgm_variants.py).
 #ifndef SGM_NT
 #define SGM_NT 3
-#endif
-#ifndef SGM_FENCE
-#define SGM_FENCE 0   // profiling builds: a scheduling fence between a step's use of its slot and the refill
 #endif
 // Fused WTA bookkeeping: 1 parks each step's S values in LDS and scans a pixel's D values in d
 // order spread over the next block's steps (no per-step lane-local argmin, no index tie-breaks
@@ -480,13 +474,13 @@ __device__ __forceinline__ void issue(const PathGeom &g, const Walker &w, const 
 {
     size_t px;
     if (SGM_WALK) {
-        px = (SGM_DIAG & 1) ? (size_t)(w.c & 63) : w.px;
+        px = w.px;
         const float2 pp = *reinterpret_cast<const float2 *>(sd.pen + px * 16 + g.ch);
         sl.p1 = pp.x;
         sl.p2 = pp.y;
     } else {
         const int r = min(max(w.r, 0), g.H - 1), c = min(max(w.c, 0), g.W - 1);
-        px = (SGM_DIAG & 1) ? (size_t)(c & 63) : (size_t)r * g.W + c;
+        px = (size_t)r * g.W + c;
         int pr = r - g.dr, pc = c - g.dc;
         const bool pin = pr >= 0 && pr < g.H && pc >= 0 && pc < g.W;
         pr = pin ? pr : r;
@@ -758,7 +752,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                     else wta_merge(mv_b, mv_a, v2, a2);
                     if (j == PF - 1) wta_block_store<G>(mv_b, mv_a, wpx[(buf ^ 1) * PF + wst], wq, sd.disp);
                 }
-            } else if (VEC && !(SGM_DIAG & 2)) {
+            } else if (VEC) {
                 // every step stores: a step that must not (past the line's end, a line gone faithful)
                 // writes the dump row instead.  A store behind a branch left the waitcnt pass unsure
                 // how many stores were in flight, so it waited for loads issued 2-3 steps back
@@ -776,7 +770,7 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
                         *reinterpret_cast<FVec<DPL> *>(sbase + dbase) = ov;
                     }
                 }
-            } else if (k < g.n && keep && !(SGM_DIAG & 2)) {
+            } else if (k < g.n && keep) {
                 {
 #pragma unroll
                     for (int i = 0; i < DPL; i++)
@@ -793,7 +787,6 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
             for (int i = 0; i < DPL; i++) L[i] = Ln[i];
             // the slot is refilled after its use (not hoisted above it): its registers are reused,
             // with no moves -- and waits -- at the loop back-edge
-            if (SGM_FENCE) __builtin_amdgcn_sched_barrier(0);
             issue<DPL, VEC, FIRST>(g, ahead, sd, D, dbase, ring[j]);
             ahead.advance(g);
         }
