@@ -65,13 +65,10 @@ static_assert(WN_RAW_INS * 64 >= WN_IY * WN_IX * 4, "raw chunks");
 
 typedef float wn_f2 __attribute__((ext_vector_type(2)));
 typedef _Float16 wn_h2 __attribute__((ext_vector_type(2)));
-constexpr uint32_t WN_OOB = 0x80000000u;
+constexpr uint32_t WN_OOB = 0x80000000u;   // a voffset past num_records: the load returns 0
 #ifndef WN_VALU_PER_MFMA
 #define WN_VALU_PER_MFMA 5
 #endif
-#ifndef WN_DIAG
-#define WN_DIAG 0   // profiling builds only (tools/tower_variants.sh): 1 no LDS-DMA, 2 no V transform, 4 no MFMAs, 8 no epilogue
-#endif   // a voffset past num_records: the load returns 0
 
 __device__ __forceinline__ void wn_tile(const XpBatch &bt, int t, int &img, int &ty0, int &tx0)
 {
@@ -223,7 +220,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
         bytes = plane_bytes - o * (IN_CB ? 64u : 256u);
     };
     auto issue = [&](int g, const float *base, uint32_t bytes) {
-        if (WN_DIAG & 1) return;
         const int cb = g & 3;
         const __amdgpu_buffer_rsrc_t rs = IN_CB ? wn_rsrc(base + (size_t)cb * Hin * Win * 16, bytes)
                                                 : wn_rsrc(base + cb * 16, bytes - 64u * cb);
@@ -277,7 +273,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
     const float sgf = half == 0 ? 1.0f : -1.0f;
     const int tstage = (chp >> 2) * WN_HALF + tl * 16 + (chp & 3) * 4;
     auto transform = [&](int g, float s) {
-        if (WN_DIAG & 2) return;
         int tr = traw;   // opaque: one address add per step, not one hoisted register per ring buffer
         asm volatile("" : "+v"(tr));
         const char *rb = wsm + WN_RAW_OFF + (size_t)(g % WN_RING) * WN_RAW_BYTES + tr;
@@ -379,7 +374,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
             // 12 MFMAs, position-major (the B fragments of one position live at a time); within a
             // position the two M-tile chains alternate, the small products l.h', h.l' first
             auto mfma = [&](int k) {
-                if (WN_DIAG & 4) return;
                 const int p = k / 6, L = (k % 6) >> 1, m = k & 1;
                 floatx16 &c = acc[p][m];
                 const WnA &a = u[p][m][cb];
@@ -409,21 +403,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
         // P_w[j][tile][cout]: lane holds tile lane & 31, couts 8q + 4 bh + e; the float4 slots of a
         // tile's 32 couts XOR-swizzled by the tile (the 8 consecutive tiles of a ds_write_b128
         // group hit 8 bank groups)
-        if (WN_DIAG & 8) {
-            if (w == 0 && lane < 32) {
-                float t = 0.f;
-#pragma unroll
-                for (int e = 0; e < 16; e++) t += acc[0][0][e] + acc[0][1][e] + acc[1][0][e] + acc[1][1][e];
-                out[img * bt.out_stride + lane] = t;
-            }
-            if (pass + 1 < npass) {
-                scales_of(pass + 1);
-                transform(4 * (pass + 1), s);
-                __builtin_amdgcn_s_waitcnt(WN_LGKM0);
-                __builtin_amdgcn_s_barrier();
-            }
-            continue;
-        }
         float *P = reinterpret_cast<float *>(wsm);
         // final phase: cout quad fq, output column j of tile ft -- 16 consecutive lanes cover two
         // adjacent pixels, a wave 16 pixels of one row: full 64-B runs of every c-block plane
