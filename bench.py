@@ -1,8 +1,9 @@
 #!/usr/bin/env python
 """bench.py -- throughput of the stereo matching hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload north_star|cones|cv]
-                    [--mode pairdp|dshard] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--workload north_star|cones|cv|c3|c4|c5|north_star_sgm]
+                    [--mode auto|pairdp|dshard|dshard_rep|rowband] [--no-cpu-baseline] [--dump-disp PATH]
 
 A step = one stereo pair through the hot path with inputs resident in HBM:
 u8 images -> z-norm + pad -> MC-CNN-fast tower (5 conv layers, f16x3 MFMA at fp32
@@ -10,7 +11,9 @@ accuracy) on both images -> fused certified cost volume + WTA over D disparities
 (bit-identical to the exact NumPy-order path) -> float32 disparity.
 Default workload: the north-star size 1024x1024, D = 192 (BASELINE.json).
 
-N > 1 (one process per GPU under torchrun, RCCL):
+N > 1 (one process per GPU under torchrun, RCCL).  The default --mode auto runs dshard (the north
+star's disparity-sharded cost volume) for `value` and times the other three schemes on the same pair
+after it (stages.multi_gpu_modes):
   pairdp : every rank matches its own pair each step (config 4) -- weak scaling,
            no collective on the data path;
   dshard : one pair per step, disparity-sharded over the ranks with the feature
@@ -55,7 +58,13 @@ WORKLOADS = {
     "c3": (2000, 3000, 256, "tower+cbca+sgm"),
     # the north-star size through the reference's whole GPU path (+ the build-defined CBCA)
     "north_star_sgm": (1024, 1024, 192, "tower+cbca+sgm"),
+    # BASELINE config 4: Middlebury-2005/2006 scale pairs, one pair per GPU (pair-DP)
+    "c4": (1110, 1390, 256, "tower+cv_wta"),
+    # BASELINE config 5: one 4K pair, D = 512 (the fused CV+WTA never materialises the 17 GB volume, so
+    # N = 1 fits one GPU; N > 1 shards it by disparity block)
+    "c5": (2160, 3840, 512, "tower+cv_wta"),
 }
+REF_GPU_PATH_MAX_VOX = 1110 * 1390 * 256   # stages.reference_gpu_path (L/R volumes + S resident) up to C4
 CBCA_ITERS, CBCA_L1, CBCA_TAU = 2, 14, 0.02
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
 PEAK_BF16_TFLOPS = 2516.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz)
@@ -163,6 +172,16 @@ def make_step(m: StereoMatcher, what: str, t_conv: Timer, t_cv: Timer, t_tower: 
     return step
 
 
+def cpu_share():
+    """Host threads the CPU baseline may use: OMP_NUM_THREADS when the launcher sets it (16 on a one-GPU
+    box), else min(16, cpu_count)."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, n if n > 0 else min(16, os.cpu_count() or 1))
+
+
 def cpu_baseline(H, W, D, what, budget_s=15.0):
     """The C oracle (exact) on a bounded sample of the same workload: one thread, then the host's CPU
     share (min(16, cpu_count): row bands on Python threads for the tower + CV/WTA path, OpenMP over
@@ -171,7 +190,10 @@ def cpu_baseline(H, W, D, what, budget_s=15.0):
     from scenedepthestimation_amd import mc_cnn
     oracle.build()
     oracle.set_threads(1)
-    nt = min(16, os.cpu_count() or 1)
+    # the box's CPU share: one GPU's box allots 16 host CPUs (OMP_NUM_THREADS=16 there), while
+    # os.cpu_count() reports the whole host's (256 on the MI355X boxes): more threads would contend
+    # with other jobs' shares rather than measure this port
+    nt = cpu_share()
     left, right, _ = stereo_pair(H, W, D, seed=0)
     w = mc_cnn.synthetic_weights(NLAYERS)
     hw, hb = mc_cnn.layer_lists(w, NLAYERS)
@@ -275,10 +297,13 @@ def numpy_baseline(H, W, D, budget_s=8.0):
     tc, ta, _ = run_cv(2)
     rows = int(max(1, min(H, budget_s / max((tc + ta) / 2, 1e-6))))
     tc, ta, cv = run_cv(rows)
-    # the Python loop on one row of the same volume (~W * D scalar steps)
+    # the Python loop on whole rows of the same volume (~W * D scalar steps each), for >= 1 s
     t0 = time.perf_counter()
-    wta1_loop(cv[:, :1])
-    tl = time.perf_counter() - t0
+    nrows = 0
+    while nrows < cv.shape[1] and (nrows == 0 or time.perf_counter() - t0 < 1.0):
+        wta1_loop(cv[:, nrows:nrows + 1])
+        nrows += 1
+    tl = (time.perf_counter() - t0) / nrows
     vox = float(W) * D
     per_cv, per_arg, per_loop = tc / (rows * vox), ta / (rows * vox), tl / vox     # seconds per voxel
     return {"value": 1e-6 / (per_cv + per_arg), "unit": "Mpixel-disparities/s", "cores": 1, "kind": "port",
@@ -288,7 +313,7 @@ def numpy_baseline(H, W, D, budget_s=8.0):
                 "what": "compute_cost_volume (NumPy) + WTA1 as the reference's per-pixel Python loop "
                         "(process_functional.py:96-113): the CPU path match_single.py:51-53 runs",
                 "ms_per_pair_estimate": (per_cv + per_loop) * H * W * D * 1e3,
-                "sample": f"loop timed on 1 row x {W} cols x D={D} ({tl:.2f} s)"},
+                "sample": f"loop timed on {nrows} row(s) x {W} cols x D={D} ({tl * nrows:.2f} s)"},
             "argmin_wta1_share": per_arg / (per_cv + per_arg),
             "sample": f"{rows} of {H} rows x {W} cols x D={D}: compute_cost_volume {tc:.1f} s + np.argmin {ta:.1f} s, "
                       f"features given"}
@@ -379,13 +404,54 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def make_mode(mode, H, W, D, what, rank, world, args, t_conv, t_cv, t_tower):
+    """-> (step, pairs_per_step, scaling, parallelism, result): one multi-GPU scheme (or the single-device
+    path, pairdp) on this rank.  The strong-scaling schemes match ONE pair (seed 0 on every rank); pair-DP
+    matches its own pair per rank (seed = rank).  result() returns the disparity map the last step made
+    (rank 0's pair for pair-DP)."""
+    if mode == "pairdp" or world == 1:
+        sgm = what == "tower+cbca+sgm"
+        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode, sgm=sgm,
+                          cbca_iters=CBCA_ITERS if sgm else 0, cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
+        left, right, _ = stereo_pair(H, W, D, seed=rank)
+        m.load_images(left, right)
+        if what == "cv_wta":
+            m.features()
+        step = make_step(m, what, t_conv, t_cv, t_tower)
+        step.matcher = m
+        res = (lambda: m.sgm_bufs["disp"][0]) if sgm else (lambda: m.disp)
+        return step, world, "weak", f"pairdp{world}", res
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    if mode == "dshard":
+        obj = DisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
+        obj.m.load_images(left, right)
+    elif mode == "dshard_rep":
+        obj = ReplicatedDisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
+        obj.load_images(left, right)
+    elif mode == "rowband":
+        obj = RowBandMatcher(H, W, D, rank, world, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
+        obj.load_images(left, right)
+    else:
+        raise ValueError(mode)
+
+    def step(timed=None):
+        e = t_tower.start() if timed == "stages" else None
+        r = obj.match()
+        if e is not None:
+            t_tower.stop(e)
+        return r
+    return step, 1, "strong", f"{mode}{world}", lambda: obj.disp
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)     # ~0.1 s timed at the north star: 10 steps (20 ms) swung 2.05-2.25 ms/pair box to box
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="north_star", choices=sorted(WORKLOADS))
-    ap.add_argument("--mode", default="pairdp", choices=["pairdp", "dshard", "dshard_rep", "rowband"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "pairdp", "dshard", "dshard_rep", "rowband"])
+    ap.add_argument("--dump-disp", default=None, help="rank 0 saves the disparity map (.npy; auto mode: also "
+                                                         "<path>.<mode>.npy for every other scheme)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3", "f16x3w"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
@@ -397,77 +463,74 @@ def main():
     # (init_from_env selected the device: cuda:LOCAL_RANK, or LOCAL_RANK mod the device count for
     # ranks sharing a GPU over gloo)
     H, W, D, what = WORKLOADS[args.workload]
-    left, right, _ = stereo_pair(H, W, D, seed=rank)
+    left, right, _ = stereo_pair(H, W, D, seed=rank)     # this rank's pair (pair-DP; rank 0: seed 0)
+    mode = args.mode
+    if mode == "auto":
+        # one GPU: the single-device hot path; N > 1: north_star's disparity-sharded cost volume
+        # (strong scaling), with the other schemes timed beside it in stages.multi_gpu_modes
+        mode = "pairdp" if world == 1 else "dshard"
+    if world > 1 and what != "tower+cv_wta" and mode != "pairdp":
+        raise SystemExit(f"--mode {mode}: the sharded schemes run the tower + CV/WTA workloads only "
+                         f"(SGM needs every disparity per step: replicas only, --mode pairdp)")
 
     t_conv, t_cv, t_tower = Timer(), Timer(), Timer()
-    if args.mode == "dshard" and world > 1:
-        dm = DisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
-        dm.m.load_images(left, right)
+    m = None
+    step, pairs_per_step, scaling, par, result = make_mode(mode, H, W, D, what, rank, world, args,
+                                                           t_conv, t_cv, t_tower)
+    if mode == "pairdp":
+        m = step.matcher
 
-        def step(timed=None):
-            e = t_tower.start() if timed == "stages" else None
-            r = dm.match()
-            if e is not None:
-                t_tower.stop(e)
-            return r
-        pairs_per_step, scaling, par = 1, "strong", f"dshard{world}"
-    elif args.mode == "dshard_rep" and world > 1:
-        dr = ReplicatedDisparityShardedMatcher(H, W, D, rank, world, tower_precision=args.tower_precision)
-        dr.load_images(left, right)
+    def timed_run(step_fn, nsteps, nwarm, timed):
+        for _ in range(nwarm):
+            step_fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step_fn(timed=timed)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        # max over ranks (gloo reduces host tensors: SDE_DIST_BACKEND=gloo runs ranks on a shared GPU)
+        tt = torch.tensor([el], dtype=torch.float64,
+                          device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
 
-        def step(timed=None):
-            e = t_tower.start() if timed == "stages" else None
-            r = dr.match()
-            if e is not None:
-                t_tower.stop(e)
-            return r
-        pairs_per_step, scaling, par = 1, "strong", f"dshard_rep{world}"
-    elif args.mode == "rowband" and world > 1:
-        rb = RowBandMatcher(H, W, D, rank, world, tower_precision=args.tower_precision, cv_mode=args.cv_mode)
-        rb.load_images(left, right)
-
-        def step(timed=None):
-            e = t_tower.start() if timed == "stages" else None
-            r = rb.match()
-            if e is not None:
-                t_tower.stop(e)
-            return r
-        pairs_per_step, scaling, par = 1, "strong", f"rowband{world}"
-    else:
-        sgm = what == "tower+cbca+sgm"
-        m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, cv_mode=args.cv_mode, sgm=sgm,
-                          cbca_iters=CBCA_ITERS if sgm else 0, cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
-        m.load_images(left, right)
-        if what == "cv_wta":
-            m.features()
-        step = make_step(m, what, t_conv, t_cv, t_tower)
-        pairs_per_step, scaling, par = world, "weak", f"pairdp{world}"
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed="conv")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_run(step, args.steps, args.warmup, "conv")
     # per-stage times from a few extra steps outside the timed region (their events would add
     # stream barriers to the timed steps)
     for _ in range(min(args.steps, 5)):
         step(timed="stages")
     torch.cuda.synchronize()
-    # max over ranks (gloo reduces host tensors: SDE_DIST_BACKEND=gloo runs ranks on a shared GPU)
-    tt = torch.tensor([elapsed], dtype=torch.float64,
-                      device="cuda" if world == 1 or dist.get_backend() == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    elapsed = float(tt.item())
+    disp_primary = result().detach().clone() if args.dump_disp else None
+
+    multi = None
+    if world > 1 and args.mode == "auto":
+        # the other multi-GPU schemes on the same pair, same ranks, same clock discipline (barrier +
+        # max over ranks); pair-DP is weak scaling (world pairs per step), the rest strong (one pair)
+        multi = {mode: {"ms_per_step": elapsed / args.steps * 1e3, "pairs_per_step": pairs_per_step,
+                        "scaling": scaling, "primary": True}}
+        others = [x for x in ("dshard", "dshard_rep", "rowband", "pairdp") if x != mode]
+        del step
+        torch.cuda.empty_cache()
+        for om in others:
+            st2, pps2, sc2, _par2, res2 = make_mode(om, H, W, D, what, rank, world, args, Timer(), Timer(), Timer())
+            n2 = min(args.steps, 10)
+            el2 = timed_run(st2, n2, min(args.warmup, 3), None)
+            multi[om] = {"ms_per_step": el2 / n2 * 1e3, "pairs_per_step": pps2, "scaling": sc2,
+                         "Mvox_s": float(H) * W * D * pps2 * n2 / el2 / 1e6}
+            if args.dump_disp and rank == 0:
+                np.save(f"{args.dump_disp}.{om}.npy", res2().cpu().numpy())
+            del st2, res2
+            torch.cuda.empty_cache()
+    if args.dump_disp and rank == 0:
+        np.save(args.dump_disp, disp_primary.cpu().numpy())
 
     vox = float(H) * W * D
     value = vox * pairs_per_step * args.steps / elapsed / 1e6
@@ -477,7 +540,7 @@ def main():
     parity = None
     host_io_ms = None
     stages = {}
-    if what == "tower+cbca+sgm" and (args.mode == "pairdp" or world == 1):
+    if what == "tower+cbca+sgm" and mode == "pairdp":
         stages["tower_ms_pair"] = t_tower.mean_ms()
         stages["gpu_path_ms"] = t_cv.mean_ms()
         tim = {}
@@ -500,7 +563,7 @@ def main():
                 "traffic": None,
                 "per_launch": f"2 sides x (8 + 5 x 12 + 8) B/voxel x {vox / 1e6:.0f} Mvox + disp = "
                               f"{sgm_bytes / 1e9:.2f} GB over {sgm_ms:.3f} ms (7 launches)"}
-    elif args.mode == "pairdp" or world == 1:
+    elif mode == "pairdp":
         cv_ms = t_cv.mean_ms()
         bytes_cv = 4.0 * H * W * 2 * NF + 4.0 * H * W
         stages["cv_wta_ms"] = cv_ms
@@ -588,13 +651,14 @@ def main():
             del cert_disp, cert_min, ex_disp, ex_min, hooked
             # the reference's default GPU path at the same size (match_single.py:49 ->
             # disparity_compute_by_gpu), + the build-defined CBCA x2: north_star's own target
-            ms_ = StereoMatcher(H, W, D, tower_precision=args.tower_precision, sgm=True, cbca_iters=CBCA_ITERS,
-                                cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
-            ms_.load_images(left, right)
-            ms_.features()
-            stages["reference_gpu_path"] = gpu_path_stages(ms_)
-            del ms_
-            torch.cuda.empty_cache()
+            if vox <= REF_GPU_PATH_MAX_VOX:
+                ms_ = StereoMatcher(H, W, D, tower_precision=args.tower_precision, sgm=True, cbca_iters=CBCA_ITERS,
+                                    cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
+                ms_.load_images(left, right)
+                ms_.features()
+                stages["reference_gpu_path"] = gpu_path_stages(ms_)
+                del ms_
+                torch.cuda.empty_cache()
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             kname = ("cv_wta_row_kernel + cv_wta_fixup_kernel (certified fused cost volume + WTA)"
@@ -606,7 +670,9 @@ def main():
                     "traffic": None,
                     "per_launch": f"{bytes_cv / 1e6:.1f} MB = 4*H*W*(2*64+1) over {cv_ms:.3f} ms" + extra}
     else:
-        stages[f"{args.mode}_step_ms"] = t_tower.mean_ms()
+        stages[f"{mode}_step_ms"] = t_tower.mean_ms()
+    if multi is not None:
+        stages["multi_gpu_modes"] = multi
 
     if roof is not None:
         tb, src = measured_traffic(args.workload)
@@ -619,6 +685,8 @@ def main():
         cpu = cpu_baseline(H, W, D, what)
         cpu["cpu_model"] = cpu_model()
         cpu["host_cpus_visible"] = os.cpu_count()
+        cpu["cores_rationale"] = ("the one-GPU box's CPU share (OMP_NUM_THREADS); os.cpu_count() counts the "
+                                  "whole host, whose other CPUs belong to other GPUs' jobs")
         if what in ("tower+cv_wta", "cv_wta"):
             cpu["numpy_restatement"] = numpy_baseline(H, W, D)
 

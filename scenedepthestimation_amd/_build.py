@@ -71,6 +71,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        # ISA lint (store-data overwrite, _isa_lint.py): a schedule that lost values on hardware
+        # is a build error, before the library is replaced
+        from . import _isa_lint
+        _isa_lint.check(objs)
         tmp = LIB + ".tmp"
         cmd = [hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -1,0 +1,125 @@
+"""Build-time ISA lint of libsde.so's gfx950 code objects.
+
+    python -m scenedepthestimation_amd._isa_lint [obj.o ...]
+
+Rule (DESIGN §3.2 "store-data overwrite"): no VALU instruction may write a VGPR that a
+vector-memory store of more than 64 bits of data (dwordx3 / dwordx4) reads, as one of the
+STORE_DATA_WINDOW instructions that follow the store (fewer than STORE_DATA_WINDOW wait states between).  LLVM's hazard recognizer inserts no wait state for this case when the
+store's soffset is a register (GCNHazardRecognizer::createsVALUHazard), yet the round-4 self-staging
+tower kernel lost exactly such values on hardware (first float of a float4, one lane pattern), and the
+shipped conv64_x6p_kernel had the same sequence (`buffer_store_dwordx4 v[180:183] ...` then
+`v_max_u32 v180, ...`).  The lint makes that schedule a build error.
+
+The device code of each object is its .hip_fatbin section (a clang offload bundle); it is unbundled
+for gfx950 and disassembled with llvm-objdump.  `s_nop N` counts N + 1 wait states, every other
+instruction one.
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+STORE_DATA_WINDOW = 2
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+
+_WIDE_STORE = re.compile(r"^(buffer|global|flat|scratch)_store_(dwordx3|dwordx4|format_xyz|format_xyzw|b96|b128)\b")
+_FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
+_REG = re.compile(r"^v(\d+)$|^v\[(\d+):(\d+)\]$")
+
+
+def _regs(tok: str):
+    m = _REG.match(tok.strip())
+    if not m:
+        return set()
+    if m.group(1) is not None:
+        return {int(m.group(1))}
+    return set(range(int(m.group(2)), int(m.group(3)) + 1))
+
+
+def _split(line: str):
+    """'  buffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen   // 000..: ...' -> (mnem, [ops])"""
+    code = line.split("//", 1)[0].strip()
+    if not code:
+        return None, []
+    parts = code.split(None, 1)
+    mnem = parts[0]
+    ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
+    return mnem, ops
+
+
+def disassemble(obj: str) -> str:
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fatbin")
+        co = os.path.join(td, "co")
+        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(td, "junk")],
+                       check=True, capture_output=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                        f"--targets={TARGET}", f"--output={co}"], check=True, capture_output=True)
+        r = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+                           text=True)
+        return r.stdout
+
+
+def lint_text(asm: str, window: int = STORE_DATA_WINDOW):
+    """Return [(function, store line, offending line, wait states)] for every violation."""
+    out = []
+    func = "?"
+    pending = []   # [(data regs, store text, wait states elapsed)]
+    for raw in asm.splitlines():
+        fm = _FUNC.match(raw.strip())
+        if fm:
+            func, pending = fm.group(1), []
+            continue
+        mnem, ops = _split(raw)
+        if mnem is None or mnem.startswith(("Disassembly", ".")) or mnem.endswith(":"):
+            continue
+        if mnem.startswith("v_") and ops:
+            dst = _regs(ops[0])
+            for data, st, ws in pending:
+                if dst & data:
+                    out.append((func, st, raw.split("//")[0].strip(), ws))
+        step = 1
+        if mnem == "s_nop" and ops:
+            try:
+                step = int(ops[0], 0) + 1
+            except ValueError:
+                step = 1
+        pending = [(d, s, w + step) for d, s, w in pending if w + step < window]
+        if _WIDE_STORE.match(mnem):
+            didx = 0 if mnem.startswith("buffer") else 1
+            if len(ops) > didx:
+                pending.append((_regs(ops[didx]), raw.split("//")[0].strip(), 0))
+    return out
+
+
+def lint_objects(objs, verbose: bool = False):
+    bad = []
+    for o in objs:
+        v = lint_text(disassemble(o))
+        if verbose:
+            print(f"isa-lint {os.path.basename(o)}: {len(v)} violation(s)", file=sys.stderr)
+        bad += [(os.path.basename(o),) + x for x in v]
+    return bad
+
+
+def check(objs) -> None:
+    bad = lint_objects(objs)
+    if bad:
+        lines = "\n".join(f"  {o}: {f}\n    {s}\n    {v}   (wait states after the store: {w})"
+                          for o, f, s, v, w in bad[:20])
+        raise RuntimeError(f"ISA lint: {len(bad)} VALU write(s) to the data VGPRs of a >64-bit store within "
+                           f"{STORE_DATA_WINDOW} wait states:\n{lines}")
+
+
+if __name__ == "__main__":
+    here = os.path.dirname(os.path.abspath(__file__))
+    objs = sys.argv[1:] or sorted(os.path.join(here, "_obj", f) for f in os.listdir(os.path.join(here, "_obj"))
+                                  if f.endswith(".o"))
+    bad = lint_objects(objs, verbose=True)
+    for o, f, s, v, w in bad:
+        print(f"{o}: {f}\n    {s}\n    {v}   [{w}]")
+    sys.exit(1 if bad else 0)

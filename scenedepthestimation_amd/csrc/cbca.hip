@@ -589,14 +589,17 @@ static inline int cb_hp(int H) { return (H + 3) & ~3; }
 
 static size_t cbca_ws_bytes(int H, int W) { return sizeof(uint32_t) * (size_t)cb_hp(H) * (size_t)W; }
 
-// Resident workgroups of a pass kernel (occupancy x CUs), per device and kernel.
+// Resident workgroups of a pass kernel (occupancy x CUs), cached per device and kernel (`cache` is
+// one slot per device id; a process driving GPUs with different CU counts sizes each grid for its own).
 template <typename K>
-static int cb_resident(K kernel, int threads = 64)
+static int cb_resident(std::atomic<int> (&cache)[64], K kernel, int threads = 64)
 {
     int dev = 0, cus = 256, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (const int c = cache[dev].load(std::memory_order_relaxed)) return c;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per <= 0) per = 8;
+    cache[dev].store(per * cus, std::memory_order_relaxed);
     return per * cus;
 }
 
@@ -625,12 +628,10 @@ static void cbca_left_iters(float *cv, float *tmp, const uint32_t *al, const uin
     v.nper = 0;
     for (int c = 0; c < v.ndc; c++) v.nper += (int64_t)max(W - 64 * c, 0);    // columns x >= 64c
     v.nitems = v.nper * v.nseg;
-    static std::atomic<int> res_h{0}, res_v{0};
-    if (!res_h.load()) res_h = cb_resident(cbca_h_kernel<R>);
-    if (!res_v.load()) res_v = cb_resident(cbca_v_kernel<R>, 64 * CbV<R>::WPB);   // workgroups
+    static std::atomic<int> res_h[64], res_v[64];
     constexpr int VW = CbV<R>::WPB;
-    const int gh = cb_grid(h.nitems, res_h.load());
-    const int gv = (cb_grid(v.nitems, res_v.load() * VW) + VW - 1) / VW;   // waves -> workgroups
+    const int gh = cb_grid(h.nitems, cb_resident(res_h, cbca_h_kernel<R>));
+    const int gv = (cb_grid(v.nitems, cb_resident(res_v, cbca_v_kernel<R>, 64 * VW) * VW) + VW - 1) / VW;   // waves -> workgroups
     h.src = cv, h.dst = tmp;
     v.src = tmp, v.dst = cv;
     for (int it = 0; it < iters; it++) {
@@ -745,7 +746,7 @@ SDE_EXPORT int sde_cbca_lr(float *cv_l, float *cv_r, float *tmp, const uint32_t 
     if (!cv_l || !cv_r || !tmp || !arms_l || !arms_r || iters < 0 || cv_l == cv_r || cv_l == tmp || cv_r == tmp ||
         !cbca_shape_ok(H, W, D, L1) || (iters > 0 && (!ws || ws_bytes < cbca_ws_bytes(H, W))))
         return SDE_ERR_ARG;
-    if (iters == 0) return SDE_OK;
+    // iters == 0 aggregates nothing but still defines cv_r as the shear of cv_l (as the oracle does)
     const int s = cbca_left(cv_l, tmp, arms_l, arms_r, H, W, D, L1, iters, ws, as_stream(stream));
     if (s != SDE_OK) return s;
     cbca_rotate(cv_l, cv_r, H, W, D, +1, true, as_stream(stream));

@@ -739,6 +739,8 @@ __device__ __forceinline__ void xp_flush_amax(uint32_t &amax_run, int &amax_img,
     amax_run = 0u;
 }
 
+constexpr int XP_PIN = 4;   // a stored float4's registers are not rewritten before XP_PIN - 1 more stores issue
+
 template <bool LAST, bool OUT_CB, bool F16, int XP_WROWS>
 __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int lane, int g, int mt0, int img,
                                             int ty0, int tx0, float unscale, const float4 *lbias4,
@@ -766,6 +768,14 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
         // else [h][w][64]
         const uint32_t vo = xok ? (uint32_t)(x * (OUT_CB ? 64 : 256) + 16 * h) : XP_OOB;
         const size_t HW = (size_t)Hout * Wout;
+        // Store-data registers stay untouched for XP_PIN stores ("store-data overwrite"):
+        // each stored float4 is pinned live by an empty asm placed after the store XP_PIN - 1 stores
+        // later, and the epilogue's last pins carry an s_nop, so no VALU writes a register a dwordx4
+        // store still reads within XP_PIN instructions -- the store's issue and its data read are not
+        // one event when MFMA waves contend for the VGPR read ports.  _isa_lint.py checks the built
+        // code objects for this schedule.
+        constexpr int NPIN = MW * 2 * XP_WROWS * 2;
+        u32x4 pin[NPIN];
 #pragma unroll
         for (int m = 0; m < MW; m++) {
             float4 b4[4];
@@ -780,29 +790,35 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
 #pragma unroll
                 for (int r = 0; r < XP_WROWS; r++) {
                     const floatx16 &c = acc[m * XP_WROWS + r];
-                    if (ty0 + row0 + r < Hout) {   // wave-uniform
-                        const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
+                    const bool rok = ty0 + row0 + r < Hout;   // wave-uniform
+                    const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
 #pragma unroll
-                        for (int ql = 0; ql < 2; ql++) {
-                            const int q = 2 * qh + ql;
-                            const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
-                            float o4[4];
+                    for (int ql = 0; ql < 2; ql++) {
+                        const int q = 2 * qh + ql;
+                        const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+                        float o4[4];
 #pragma unroll
-                            for (int e = 0; e < 4; e++)
-                                o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]),
-                                              0.f);
-                            const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
-                            if (F16) {
+                        for (int e = 0; e < 4; e++)
+                            o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]), 0.f);
+                        const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                        const int k = ((m * 2 + qh) * XP_WROWS + r) * 2 + ql;
+                        pin[k] = __builtin_bit_cast(u32x4, o);
+                        if (rok) {
+                            if (F16) {   // the bound before the store: nothing writes o's registers after it
                                 amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
                                 amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
                             }
                             // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
                             xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
                         }
+                        if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
                     }
                 }
             }
         }
+#pragma unroll
+        for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
+        asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
         if (F16) {
             if (!xok) amax = 0u;   // lanes past the output edge stored nothing
             // one atomic per wave and image (flushed when the tiles move to the next

@@ -219,8 +219,14 @@ class StereoMatcher:
             self.sgm_bufs["cbca_ws"] = torch.empty((ops.cbca_workspace_bytes(H, W),), dtype=torch.uint8, device=dev)
 
     def cbca(self, cv_l, cv_r, img_l, img_r):
-        """Cross-based aggregation of the L/R [H,W,D] volumes in place (build-defined).
-        Arms come from the z-normalised images (the tower's input normalisation)."""
+        """Cross-based aggregation (build-defined) of the left [H,W,D] volume in
+        place, and the right volume derived from it.  Arms come from the z-normalised images (the
+        tower's input normalisation).
+
+        cv_r is an OUTPUT: its valid voxels (x + d < W) are overwritten with the shear of the aggregated
+        cv_l and their input is never read -- correct only because the GPU path's right volume IS the
+        left one's shear (one sweep computes each voxel once, sec. 3.1).  Its invalid voxels are kept.
+        For two independent volumes use ops.cbca_pair."""
         if self.sgm_bufs is None or "arms" not in self.sgm_bufs:
             saved, self.cbca_iters = self.cbca_iters, max(self.cbca_iters, 1)
             self._alloc_sgm()

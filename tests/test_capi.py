@@ -169,3 +169,32 @@ def test_ops_refuse_cpu_tensors():
         ops.cv_wta(f, f, 0, 2)
     with pytest.raises(ValueError, match="GPU"):
         ops.cost_volume(f, f, 2)
+
+
+def test_isa_lint_flags_store_data_overwrite():
+    """The lint catches the round-4 schedule (a VALU write into a dwordx4 store's data right after
+    it) and accepts it once the write is two instructions away or aimed elsewhere."""
+    from scenedepthestimation_amd import _isa_lint
+    head = "0000000000001000 <k>:\n"
+    bad = head + ("\tbuffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen // 000000001000: x\n"
+                  "\tv_max_u32_e32 v180, v176, v177 // 000000001008: x\n")
+    near = head + ("\tbuffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen\n"
+                   "\tv_mov_b32_e32 v1, v2\n\tv_lshlrev_b32_e32 v183, 2, v208\n")
+    nop = head + ("\tglobal_store_dwordx4 v[0:1], v[4:7], off\n\ts_nop 1\n\tv_mov_b32_e32 v5, v2\n")
+    far = head + ("\tbuffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen\n"
+                  "\tv_mov_b32_e32 v1, v2\n\ts_nop 0\n\tv_max_u32_e32 v180, v176, v177\n")
+    other = head + ("\tbuffer_store_dwordx2 v[180:181], v206, s[28:31], s68 offen\n\tv_mov_b32_e32 v180, v2\n")
+    assert len(_isa_lint.lint_text(bad)) == 1
+    assert len(_isa_lint.lint_text(near)) == 1
+    assert _isa_lint.lint_text(nop) == []
+    assert _isa_lint.lint_text(far) == []
+    assert _isa_lint.lint_text(other) == []
+
+
+def test_isa_lint_passes_on_the_built_library():
+    from scenedepthestimation_amd import _isa_lint
+    from scenedepthestimation_amd._build import OBJ
+    objs = sorted(os.path.join(OBJ, f) for f in os.listdir(OBJ) if f.endswith(".o"))
+    if not objs or not os.path.exists(_isa_lint.LLVM):
+        pytest.skip("no built objects / ROCm LLVM tools")
+    assert _isa_lint.lint_objects(objs) == []

@@ -50,19 +50,33 @@ def test_multirank_classes_on_one_gpu(gpu, world, H, W, D):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,scaling", [("pairdp", "weak"), ("dshard", "strong"), ("dshard_rep", "strong"),
-                                          ("rowband", "strong")])
-def test_bench_multirank_modes_on_one_gpu(gpu, mode, scaling):
+@pytest.mark.parametrize("mode,primary,scaling", [("auto", "dshard", "strong"), ("pairdp", "pairdp", "weak"),
+                                                  ("dshard", "dshard", "strong"),
+                                                  ("dshard_rep", "dshard_rep", "strong"),
+                                                  ("rowband", "rowband", "strong")])
+def test_bench_multirank_modes_on_one_gpu(gpu, tmp_path, mode, primary, scaling):
     """bench.py --gpus 2 exactly as the driver's scaling run launches it (torch.distributed.run, one
     process per rank), here both ranks on the box's one GPU over gloo (SDE_DIST_BACKEND=gloo; on an
     8-GPU node the same code runs one rank per GPU over RCCL): every mode the scaling run can use
-    must come back with one JSON line whose n_gpus, scaling and parallelism say what ran."""
+    must come back with one JSON line whose n_gpus, scaling and parallelism say what ran, and its
+    disparity map (rank 0's pair) must equal the single-device StereoMatcher's bit for bit.  The default
+    (auto) line is the disparity-sharded scheme, with the other three schemes timed in its stages and
+    their maps checked too."""
     import json
+
+    import numpy as np
+    import torch
+
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
     port = _free_port()
     env = dict(os.environ, SDE_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dump = str(tmp_path / "disp.npy")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mode", mode,
-           "--workload", "cones", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--workload", "cones", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dump-disp", dump]
+    if mode != "auto":
+        cmd += ["--mode", mode]
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
     if p.returncode != 0:
         print(p.stdout[-3000:], "\n---- stderr ----\n", "\n".join(l for l in p.stderr.splitlines() if "Gloo" not in l)[-6000:])
@@ -71,5 +85,19 @@ def test_bench_multirank_modes_on_one_gpu(gpu, mode, scaling):
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == scaling
-    assert line["config"]["parallelism"] == f"{mode}2"
+    assert line["config"]["parallelism"] == f"{primary}2"
     assert line["value"] > 0 and line["steps"] == 2
+    H, W, D = 375, 450, 64          # bench.py's cones workload
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    m = StereoMatcher(H, W, D)
+    m.load_images(left, right)
+    want = m.match().cpu().numpy()
+    assert np.array_equal(np.load(dump), want), f"{primary}: map differs from the single-device one"
+    if mode == "auto":
+        modes = line["stages"]["multi_gpu_modes"]
+        assert set(modes) == {"dshard", "dshard_rep", "rowband", "pairdp"} and modes["dshard"]["primary"]
+        for om in ("dshard_rep", "rowband", "pairdp"):
+            assert modes[om]["ms_per_step"] > 0
+            assert np.array_equal(np.load(f"{dump}.{om}.npy"), want), f"{om}: map differs from the single-device one"
+    del m
+    torch.cuda.empty_cache()

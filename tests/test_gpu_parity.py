@@ -374,7 +374,8 @@ def _sheared_pair(rng, H, W, D, scale=1.0, offset=0.0):
 
 
 @pytest.mark.parametrize("H,W,D,L1,iters", [(23, 61, 40, 14, 2), (16, 96, 192, 14, 2), (40, 33, 130, 16, 1),
-                                             (70, 12, 7, 32, 2), (270, 300, 66, 14, 2), (3, 2, 16, 14, 1)])
+                                             (70, 12, 7, 32, 2), (270, 300, 66, 14, 2), (3, 2, 16, 14, 1),
+                                             (23, 61, 40, 14, 0), (16, 96, 192, 14, 0)])
 def test_cbca_lr_bit_exact(gpu, oracle, H, W, D, L1, iters):
     """The GPU path's pair: one volume aggregated + the shear == the oracle's sdeo_cbca_lr, and (the
     right volume being the left one's shear) == aggregating both volumes (cbca_pair)."""
@@ -384,7 +385,11 @@ def test_cbca_lr_bit_exact(gpu, oracle, H, W, D, L1, iters):
     al, ar = oracle.cbca_arms(il, L1, 0.03), oracle.cbca_arms(ir, L1, 0.03)
     cl, cr = _sheared_pair(rng, H, W, D, 2.0, 3.0)
     want_l, want_r = oracle.cbca_lr(cl, cr, al, ar, iters, L1=L1)
-    gl, gr = dev(cl), dev(cr)
+    # cv_r is an output (its valid voxels are never read): hand in garbage there
+    cr_in = cr.copy()
+    for d in range(min(D, W)):
+        cr_in[:, :W - d, d] = -7.5
+    gl, gr = dev(cl), dev(cr_in)
     ops.cbca_lr(gl, gr, dev(al.view(np.int32)), dev(ar.view(np.int32)), L1, iters)
     assert host(gl).tobytes() == want_l.tobytes()
     assert host(gr).tobytes() == want_r.tobytes()
