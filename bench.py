@@ -126,6 +126,8 @@ TOWER_ARITH = {
     "f16x3": "f16x3: fp32 operands scaled by powers of two and split exactly into 2 fp16 parts, 3 leading partial "
              "products on f16 MFMA, fp32 accumulation (~2^-22 per product; fp32-level error, checked vs the fp32 "
              "MFMA tower in stages)",
+    "f16x3m32": "f16x3 arithmetic with layers 3..L on the v_mfma_f32_32x32x16_f16 direct kernel (the default f16x3 "
+                "runs them on v_mfma_f32_16x16x32_f16)",
     "f16x3w": "f16x3 arithmetic with Winograd F(2x2,3x3) for layers 3..L: V = B^T d B in fp32 split into 2 fp16 "
               "parts, U = G g G^T formed in fp64 on the host and split, 3 partial products per Winograd product "
               "(2.25x fewer than direct), fp32 accumulation and output transform (fp32-level error)",
@@ -453,7 +455,7 @@ def main():
     ap.add_argument("--dump-disp", default=None, help="rank 0 saves the disparity map (.npy; auto mode: also "
                                                          "<path>.<mode>.npy for every other scheme)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3", "f16x3w"])
+    ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3", "f16x3w", "f16x3m32"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
     args = ap.parse_args()
 
@@ -583,7 +585,7 @@ def main():
             stages["tower_ms_pair"] = t_tower.mean_ms()
             stages["conv_layer3_ms"] = conv_ms
             stages["conv_fp32_equiv_TFLOPs"] = fl / (conv_ms * 1e-3) / 1e12
-            if m.tower_precision in ("bf16x6", "f16x3", "f16x3w"):
+            if m.tower_precision in ("bf16x6", "f16x3", "f16x3w", "f16x3m32"):
                 # 6 bf16 / 3 f16 partial products per fp32 product: the roof is the dense bf16/f16 MFMA rate
                 # (Winograd: 3 per Winograd product, 16 per 2x2 outputs instead of 36)
                 k, kt = (6, "bf16") if m.tower_precision == "bf16x6" else (3, "f16")
@@ -591,6 +593,7 @@ def main():
                     k = 3 * 16 / 36
                 ach = k * fl / (conv_ms * 1e-3) / 1e12
                 kname = ("wino_kernel<false,true,true>" if m.tower_precision == "f16x3w" else
+                         "conv64_h16_kernel<false,true,true,false>" if m.tower_precision == "f16x3" else
                          f"conv64_x6p_kernel<false,false,true,true,{str(kt == 'f16').lower()}>")
                 roof = {"kernel": f"{kname} (tower layer 3, {m.tower_precision})", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,

@@ -150,6 +150,10 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
  * instead of the direct 3x3 kernel (same arithmetic contract and error class, 2.25x fewer MFMA
  * products, more VALU; slower than the direct kernel at 1024^2 on MI355X -- DESIGN.md 3.2). */
 #define SDE_TOWER_WINOGRAD 16
+/* With SDE_TOWER_F16X3 only: run the 64 -> 64 layers on the v_mfma_f32_32x32x16_f16 direct kernel instead of
+ * the default v_mfma_f32_16x16x32_f16 one (same arithmetic contract).  Layers whose last-layer
+ * epilogue writes the split planes always take the 32x32x16 kernel. */
+#define SDE_TOWER_MFMA32 32
 #define SDE_TOWER_IN_CBLOCK 2
 #define SDE_TOWER_OUT_CBLOCK 4
 

@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
 }  // namespace sde
 #include "tower_wino.h"
+#include "tower_h16.h"
 namespace sde {
 
 
@@ -1383,6 +1384,17 @@ static void set_tower_attrs()
     SDE_X6P_ATTR(false, true, false, false);
 #undef SDE_X6P_ATTR1
 #undef SDE_X6P_ATTR
+#define SDE_H16_ATTR(L, I, O, S) (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<L, I, O, S>, \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM)
+    SDE_H16_ATTR(true, true, false, false);
+    SDE_H16_ATTR(true, false, false, false);
+    SDE_H16_ATTR(true, true, false, true);
+    SDE_H16_ATTR(true, false, false, true);
+    SDE_H16_ATTR(false, true, true, false);
+    SDE_H16_ATTR(false, true, false, false);
+    SDE_H16_ATTR(false, false, true, false);
+    SDE_H16_ATTR(false, false, false, false);
+#undef SDE_H16_ATTR
 #define SDE_WINO_ATTR(L, I, O) (void)hipFuncSetAttribute((const void *)wino_kernel<L, I, O>, \
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, WN_SMEM)
     SDE_WINO_ATTR(true, true, false);
@@ -1451,6 +1463,28 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 #undef SDE_WINO
         return;
     }
+    if (f16 && layer >= 3 && !(flags & SDE_TOWER_MFMA32)) {
+        // the 64 -> 64 layers on v_mfma_f32_16x16x32_f16 (tower_h16.h; same tiles as the direct kernel)
+        XpBatch bt;
+        bt.tiles_x = cdiv(wout, XP_TX);
+        bt.tiles_img = bt.tiles_x * cdiv(hout, XP_TY);
+        bt.ntiles = bt.tiles_img * nimg;
+        bt.in_stride = in_stride;
+        bt.out_stride = out_stride;
+        bt.pix_stride = (int64_t)hout * wout;
+        bt.amax_stride = amax_stride;
+        const int grid = std::min(bt.ntiles, cu_count());
+#define SDE_H16(L, I, O, S) conv64_h16_kernel<L, I, O, S><<<grid, 512, H16_SMEM, st>>>(in, Hin, Win, wk, out, hout, wout, \
+                                                                                       (S) ? ohi : nullptr, (S) ? olo : nullptr, \
+                                                                                       (S) ? onrm : nullptr, bt, in_amax, out_amax)
+        const bool split = ohi || olo || onrm;
+        if (last && split) { if (in_cb) SDE_H16(true, true, false, true); else SDE_H16(true, false, false, true); }
+        else if (last) { if (in_cb) SDE_H16(true, true, false, false); else SDE_H16(true, false, false, false); }
+        else if (in_cb) { if (out_cb) SDE_H16(false, true, true, false); else SDE_H16(false, true, false, false); }
+        else { if (out_cb) SDE_H16(false, false, true, false); else SDE_H16(false, false, false, false); }
+#undef SDE_H16
+        return;
+    }
     if (x6) {
         XpBatch bt;
         bt.tiles_x = cdiv(wout, XP_TX);
@@ -1500,9 +1534,9 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 
 static bool tower_flags_ok(int flags, bool layer_api)
 {
-    if (flags & SDE_TOWER_WINOGRAD) {   // F16X3 only: Winograd F(2x2, 3x3) for the 64 -> 64 layers
-        if (!(flags & SDE_TOWER_F16X3)) return false;
-        flags &= ~SDE_TOWER_WINOGRAD;
+    if (flags & (SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32)) {   // F16X3 only: the 64 -> 64 layers' kernel choice
+        if (!(flags & SDE_TOWER_F16X3) || (flags & SDE_TOWER_WINOGRAD && flags & SDE_TOWER_MFMA32)) return false;
+        flags &= ~(SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32);
     }
     const int prec = flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3);
     if (prec == (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) return false;

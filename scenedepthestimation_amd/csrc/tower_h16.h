@@ -1,0 +1,394 @@
+// tower_h16.h -- the MC-CNN tower's 64 -> 64 layers (3..L; mc_cnn_brunch.py:31-48, conv :70-92) as
+// a direct 3x3 implicit GEMM on v_mfma_f32_16x16x32_f16 (included by tower.hip; f16x3 arithmetic).
+//
+// Same arithmetic contract as conv64_x6p_kernel's F16 path: weights scaled by 2^tau on the host,
+// activations by 2^sigma (from the input's bound word) on the device, each split exactly into two
+// fp16 parts, the three leading partial products lo*hi + hi*lo + hi*hi accumulated in fp32 (small
+// terms first), the accumulator unscaled by 2^-(tau+sigma) (exact) in the epilogue.  Why a second
+// kernel: MI355X holds a lower clock under dense 32x32x16 MFMA streams than under 16x16x32 ones at
+// equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7: 1.12-1.15x the FLOP/s on
+// random operands), and the tower is clock-bound.
+//
+// Mapping (M = 64 output channels as 4 quarters of 16, N = pixels, K = 32 input channels of one
+// c-block x one tap x one partial product):
+// * persistent 512-thread workgroups over the batch's 16 x 32 output tiles; waves 0-3 are MFMA
+//   waves (wave g owns output rows 4g .. 4g+3, all 32 columns as two 16-pixel halves, all 64
+//   channels: 4 rows x 2 halves x 4 quarters = 32 accumulators of 4 VGPRs); waves 4-7 stage;
+// * a tile is 2 c-blocks of 32 input channels; the stagers fill a stage of 8 planes (part 2 x
+//   channel-quarter 4, 612 pixels x 8 fp16 each, planes 256-B aligned) one c-block ahead, double
+//   buffered (2 x 78 KB), one barrier per c-block;
+// * B fragment of (tap, row, half): lane l reads plane (part, l >> 4) at pixel (row + ky,
+//   16 half + (l & 15) + kx): one conflict-free ds_read_b128, a per-lane base plus an immediate;
+// * A fragments come straight from the F16 weight blob's [mtile][cblock16][tap][part][lane][8]
+//   layout (no new packing): lane l of quarter q reads 16 B at a per-lane offset, two half-taps
+//   (2 quarters each) ahead, from L2;
+// * epilogue: a lane holds channels 16q + 4(l >> 4) .. +3 of pixel (l & 15): one dwordx4 store
+//   per (row, half, quarter); the c-block-major output [cblk16][h][w][16] is written as 1 KB
+//   runs; the last layer L2-normalises over the 4 lanes x 4 quarters that hold a pixel.
+#pragma once
+
+namespace sde {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int H16_PLANE = 9984;                           // 612 pixels x 16 B, rounded up to 256 B
+constexpr int H16_STAGE = 8 * H16_PLANE;                  // [part 2][quarter 4] planes: 79,872 B
+constexpr size_t H16_BIAS_OFF = 2 * (size_t)H16_STAGE;
+constexpr size_t H16_SMEM = H16_BIAS_OFF + NF * sizeof(float);   // 160,000 B
+constexpr int H16_NCB = 2;                                // 32-channel c-blocks per tile
+constexpr int H16_HT = 18;                                // half-taps per c-block (9 taps x 2 quarter pairs)
+constexpr int H16_RD = 3;                                 // B ring depth (fragments read RD-1 steps ahead)
+static_assert(H16_PLANE >= XP_NPIX * 16 && H16_PLANE % 256 == 0, "plane size / bank alignment");
+static_assert(H16_SMEM <= 163840, "LDS");
+
+// Split 4 channels (chunk u & 3 of 16-channel half h of the 32-channel c-block) of pixel u >> 2,
+// scaled by s, into the stage's (part, quarter) planes.
+__device__ __forceinline__ void h16_put(char *sb, int h, int u, float4 v, float s)
+{
+    const int px = u >> 2, chunk = u & 3;
+    f16x4 p0, p1;
+    const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const _Float16 hh = (_Float16)xs[e];
+        p0[e] = hh;
+        p1[e] = (_Float16)(xs[e] - (float)hh);
+    }
+    char *dst = sb + (2 * h + (chunk >> 1)) * H16_PLANE + px * 16 + (chunk & 1) * 8;
+    *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
+    *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, p1);
+}
+
+// Stager waves: half-steps k = (tile, 16-channel block cb16 = k % 4) in the MFMA waves' order; half-steps
+// 2i, 2i+1 make c-block step i (stage i & 1).  Two register sets of one half-step each are loaded
+// one c-block step ahead of their store.  One barrier per c-block step, like the MFMA waves.
+template <bool IN_CB>
+__device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restrict__ in, int Hin, int Win,
+                                                const XpBatch &bt, int st, const float *__restrict__ in_amax,
+                                                const float *__restrict__ hdr)
+{
+    const int tile0 = blockIdx.x, gstride = gridDim.x;
+    const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * H16_NCB;
+    const int nh = 2 * nsteps;
+    auto load = [&](float4 (&v)[XP_UPT], int k) {
+        const int t = tile0 + (k >> 2) * gstride, cb16 = k & 3;
+        int img, ty0, tx0;
+        xp_tile(bt, t, img, ty0, tx0);
+        const float *src = in + img * bt.in_stride;
+#pragma unroll
+        for (int i = 0; i < XP_UPT; i++) {
+            const int u = st + i * XP_STAGERS;
+            v[i] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb16, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    int sc_img = -1;
+    float s = 1.0f, unscale = 1.0f;
+    auto store = [&](const float4 (&v)[XP_UPT], int k) {
+        const int im = (tile0 + (k >> 2) * gstride) / bt.tiles_img;
+        if (im != sc_img) {   // the tile's image changed: its bound word (tiles run image-major)
+            xp_scales(false, in_amax + im * bt.amax_stride, hdr, s, unscale);
+            sc_img = im;
+        }
+        char *sb = hsm + ((k >> 1) & 1) * H16_STAGE;
+#pragma unroll
+        for (int i = 0; i < XP_UPT; i++) {
+            const int u = st + i * XP_STAGERS;
+            if (u < XP_UNITS) h16_put(sb, k & 1, u, v[i], s);
+        }
+    };
+    float4 ra[XP_UPT], rb[XP_UPT];
+    load(ra, 0);
+    load(rb, 1);
+    store(ra, 0);
+    store(rb, 1);
+    if (2 < nh) load(ra, 2);
+    if (3 < nh) load(rb, 3);
+    __syncthreads();
+    // step i: the MFMA waves consume stage i & 1; here step i+1's halves are stored and step
+    // i+2's loaded
+#pragma unroll 1
+    for (int i = 0; i < nsteps; i++) {
+        if (2 * i + 2 < nh) store(ra, 2 * i + 2);
+        if (2 * i + 4 < nh) load(ra, 2 * i + 4);
+        if (2 * i + 3 < nh) store(rb, 2 * i + 3);
+        if (2 * i + 5 < nh) load(rb, 2 * i + 5);
+        __syncthreads();
+    }
+}
+
+// A fragments of one half-tap (tap s >> 1, quarters 2 (s & 1) + qq) of 32-channel c-block cb:
+// [part][qq].  aoff = the lane's offset in the F16 blob's A-fragment order (uint4 units, qq = 0).
+struct H16A {
+    f16x8 f[2][2];
+};
+
+__device__ __forceinline__ H16A h16_afrag(const uint4 *__restrict__ wf, int cb, int s, int aoff)
+{
+    const int tap = s >> 1, hf = s & 1;
+    H16A a;
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++)
+            a.f[p][qq] = __builtin_bit_cast(f16x8, wf[((((hf * XP_NCB + 2 * cb) * 9 + tap) * 2 + p) * 64) + aoff + 16 * qq]);
+    return a;
+}
+
+struct H16B {
+    f16x8 hi, lo;
+};
+
+// B fragment of step b = (half-tap b >> 3, row (b >> 1) & 3, pixel half b & 1); sb = the stage at the
+// lane's base.
+__device__ __forceinline__ H16B h16_bfrag(const char *sb, int b)
+{
+    const int tap = b >> 4, r = (b >> 1) & 3, ph = b & 1;
+    const int off = ((r + tap / 3) * XP_IX + 16 * ph + tap % 3) * 16;
+    H16B f;
+    f.hi = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + off));
+    f.lo = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + 4 * H16_PLANE + off));
+    return f;
+}
+
+__device__ __forceinline__ floatx4 mfma16(f16x8 a, f16x8 b, floatx4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// One 32-channel c-block for one MFMA wave: 18 half-taps x 8 (row, half) steps, 6 MFMAs each.
+// acc[(r * 2 + ph) * 4 + q].  a = A(cb, 0), an[k] = A(cb, 1 + k) on entry; A(ncb, 0..) on exit.
+__device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A &a, H16A (&an)[2], const uint4 *__restrict__ wf,
+                                           int cb, int ncb, int aoff, const char *sb)
+{
+    constexpr int NB = H16_HT * 8;
+    H16B ring[H16_RD];
+#pragma unroll
+    for (int k = 0; k < H16_RD - 1; k++) ring[k] = h16_bfrag(sb, k);
+#pragma unroll
+    for (int s = 0; s < H16_HT; s++) {
+        if (s > 0) {
+            a = an[0];
+            an[0] = an[1];
+            an[1] = s + 2 < H16_HT ? h16_afrag(wf, cb, s + 2, aoff) : h16_afrag(wf, ncb, s + 2 - H16_HT, aoff);
+        }
+        const int hf = s & 1;
+#pragma unroll
+        for (int rp = 0; rp < 8; rp++) {
+            const int b = s * 8 + rp;
+            __builtin_amdgcn_sched_barrier(0);
+            const H16B &bf = ring[b % H16_RD];
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) {
+                floatx4 &c = acc[rp * 4 + 2 * hf + qq];
+                c = mfma16(a.f[1][qq], bf.hi, c);
+                c = mfma16(a.f[0][qq], bf.lo, c);
+                c = mfma16(a.f[0][qq], bf.hi, c);
+            }
+            if (b + H16_RD - 1 < NB) ring[(b + H16_RD - 1) % H16_RD] = h16_bfrag(sb, b + H16_RD - 1);
+        }
+    }
+    a = an[0];
+    an[0] = an[1];
+    an[1] = h16_afrag(wf, ncb, 2, aoff);
+}
+
+// Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
+// (+ the running bound word), or (LAST) the L2 norm and [h][w][64] stores.  Stored registers are
+// pinned live for XP_PIN stores, as in xp_epilogue ("store-data overwrite").
+template <bool LAST, bool OUT_CB, bool SPLIT>
+__device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane, int g, int img, int ty0, int tx0,
+                                             float unscale, const float4 *lbias4, float *__restrict__ out, int Hout,
+                                             int Wout, const XpBatch &bt, uint16_t *__restrict__ ohi,
+                                             uint16_t *__restrict__ olo, float *__restrict__ onrm,
+                                             uint32_t &amax_run, int &amax_img, float *__restrict__ out_amax)
+{
+    int j = lane & 15, k4 = lane >> 4;
+    asm volatile("" : "+v"(j), "+v"(k4));
+    const int row0 = 4 * g;
+    constexpr int NPIN = 32;
+    u32x4 pin[NPIN];
+    if (!LAST) {
+        uint32_t amax = 0u;
+        float *const outi = out + img * bt.out_stride;
+        const size_t HW = (size_t)Hout * Wout;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float4 b4 = lbias4[4 * q + k4];
+            const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+            // OUT_CB: [cblk16 = q][h][w][16], one descriptor per c-block plane; else [h][w][64]
+            const __amdgpu_buffer_rsrc_t rs = xp_rsrc(OUT_CB ? outi + ((size_t)q * HW + (size_t)ty0 * Wout) * 16
+                                                             : outi + (size_t)ty0 * Wout * NF);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const bool rok = ty0 + row0 + r < Hout;   // wave-uniform
+                const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
+#pragma unroll
+                for (int ph = 0; ph < 2; ph++) {
+                    const int x = tx0 + 16 * ph + j;
+                    const bool xok = x < Wout;
+                    const floatx4 &c = acc[(r * 2 + ph) * 4 + q];
+                    float o4[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) o4[e] = fmaxf(fmaf(c[e], unscale, bq[e]), 0.f);
+                    const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
+                    const int k = (q * 4 + r) * 2 + ph;
+                    pin[k] = __builtin_bit_cast(u32x4, o);
+                    if (rok) {
+                        if (xok) {   // the bound before the store: nothing writes o's registers after it
+                            amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                            amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                        }
+                        xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
+                               so);
+                    }
+                    if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
+        asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+        // one atomic per wave and image (flushed when the tiles move to the next image and at the end)
+        if (img != amax_img) {
+            xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+            amax_img = img;
+        }
+        amax_run = max(amax_run, amax);
+    } else {
+        // a pixel's 64 channels: 4 quarters x 4 lanes (k4) x 4 registers of this wave
+        const size_t pix0 = (size_t)img * bt.pix_stride + (size_t)ty0 * Wout;
+        const __amdgpu_buffer_rsrc_t rs = xp_rsrc(out + pix0 * NF);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool rok = ty0 + row0 + r < Hout;
+            const uint32_t so = (uint32_t)((row0 + r) * Wout) * 256u;
+#pragma unroll
+            for (int ph = 0; ph < 2; ph++) {
+                const int x = tx0 + 16 * ph + j;
+                int kr = k4;
+                asm volatile("" : "+v"(kr));   // per-step opaque copy: bias re-read from LDS per use
+                float t[4][4];
+                float ss = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 b4 = lbias4[4 * q + kr];
+                    const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+                    const floatx4 &c = acc[(r * 2 + ph) * 4 + q];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        t[q][e] = fmaf(c[e], unscale, bq[e]);
+                        ss += t[q][e] * t[q][e];
+                    }
+                }
+                ss += __shfl_xor(ss, 16, 64);
+                ss += __shfl_xor(ss, 32, 64);
+                const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+                const bool xok = x < Wout;
+                const uint32_t vo = xok ? (uint32_t)(x * 256 + 16 * k4) : XP_OOB;
+                float s2 = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 o = make_float4(t[q][0] * inv, t[q][1] * inv, t[q][2] * inv, t[q][3] * inv);
+                    const int k = (r * 2 + ph) * 4 + q;
+                    pin[k] = __builtin_bit_cast(u32x4, o);
+                    if (rok) xp_st4(o, rs, vo + 64u * q, so);
+                    if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
+                    if (SPLIT) {   // bf16 split planes of the features (sde_cv_wta_split's input)
+                        const float xs[4] = {o.x, o.y, o.z, o.w};
+                        bf16x4 hv, lv;
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            const __bf16 hh = (__bf16)xs[e];
+                            hv[e] = hh;
+                            lv[e] = (__bf16)(xs[e] - (float)hh);
+                            s2 += xs[e] * xs[e];
+                        }
+                        if (rok) {
+                            const __amdgpu_buffer_rsrc_t rh = xp_rsrc(ohi + pix0 * NF), rl = xp_rsrc(olo + pix0 * NF);
+                            const uint32_t o2 = xok ? (uint32_t)(x * 128 + 32 * q + 8 * k4) : XP_OOB;
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rh, o2, so / 2u, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lv), rl, o2, so / 2u, 0);
+                        }
+                    }
+                }
+                if (SPLIT && onrm) {   // fp32 rounding bound of the 64-term sum
+                    s2 += __shfl_xor(s2, 16, 64);
+                    s2 += __shfl_xor(s2, 32, 64);
+                    if (rok) {
+                        const __amdgpu_buffer_rsrc_t rn = xp_rsrc(onrm + pix0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sqrtf(s2) * 1.000004f), rn,
+                                                              (xok && k4 == 0) ? (uint32_t)(x * 4) : XP_OOB, so / 64u, 0);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
+        asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+    }
+}
+
+// Layers 3..L, f16x3; IN_CB / OUT_CB: c-block-major activations [cblk16][h][w][16] (the tower's
+// intermediate layout) or [h][w][64]; LAST writes the [h][w][64] features (+ the optional split
+// planes and norm bounds: SPLIT, the last layer only).
+template <bool LAST, bool IN_CB, bool OUT_CB, bool SPLIT>
+__global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict__ in, int Hin, int Win,
+                                                         const float *__restrict__ wkblob, float *__restrict__ out,
+                                                         int Hout, int Wout, uint16_t *__restrict__ ohi,
+                                                         uint16_t *__restrict__ olo, float *__restrict__ onrm, XpBatch bt,
+                                                         const float *__restrict__ in_amax, float *__restrict__ out_amax)
+{
+    extern __shared__ __attribute__((aligned(16))) char hsm[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    int tile = blockIdx.x;
+    if (tile >= bt.ntiles) return;
+    const float *hdr = wkblob + LK_F16 + LK_W;
+    if (wave >= 4) {
+        h16_stager_loop<IN_CB>(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr);
+        return;
+    }
+    const int g = __builtin_amdgcn_readfirstlane(wave);
+    float *lbias = reinterpret_cast<float *>(hsm + H16_BIAS_OFF);
+    if (wave == 0) lbias[lane] = wkblob[lane];   // published by the first barrier below
+    const float4 *lbias4 = reinterpret_cast<const float4 *>(lbias);
+    const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + LK_F16);
+    // the lane's A-fragment offset: cb16 = 2 cb + (lane >> 5), channel half (lane >> 4) & 1, n & 15
+    const int aoff = (lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15);
+    // the lane's B base: plane quarter lane >> 4, pixel (4g, lane & 15) of the input tile
+    const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
+    H16A a = h16_afrag(wf, 0, 0, aoff), an[2] = {h16_afrag(wf, 0, 1, aoff), h16_afrag(wf, 0, 2, aoff)};
+    __syncthreads();
+
+    int sc_img = -1;
+    float sc_u = 1.0f;
+    uint32_t amax_run = 0u;
+    int amax_img = -1;
+    int cur = 0;
+    for (; tile < bt.ntiles; tile += gridDim.x) {
+        int img, ty0, tx0;
+        xp_tile(bt, tile, img, ty0, tx0);
+        floatx4 acc[32];
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int cb = 0; cb < H16_NCB; cb++) {
+            h16_cblock(acc, a, an, wf, cb, cb ^ 1, aoff, hsm + cur * H16_STAGE + bbase);
+            if (cb == H16_NCB - 1) {
+                if (img != sc_img) {
+                    float s_unused;
+                    xp_scales(false, in_amax + img * bt.amax_stride, hdr, s_unused, sc_u);
+                    sc_img = img;
+                }
+                h16_epilogue<LAST, OUT_CB, SPLIT>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi, olo,
+                                           onrm, amax_run, amax_img, out_amax);
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+    }
+    if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+}
+
+}  // namespace sde

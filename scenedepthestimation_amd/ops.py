@@ -216,8 +216,11 @@ def tower_workspace_bytes(H: int, W: int, nlayers: int, nf: int = 64) -> int:
 
 
 # "f16x3w": f16x3 with the Winograd F(2x2, 3x3) kernel for layers 3..L (SDE_TOWER_WINOGRAD)
+# "f16x3m32": f16x3 with layers 3..L on the 32x32x16 direct kernel (SDE_TOWER_MFMA32; the default f16x3
+# runs them on the 16x16x32 kernel)
 TOWER_PRECISIONS = {"fp32": _lib.SDE_TOWER_FP32, "bf16x6": _lib.SDE_TOWER_BF16X6, "f16x3": _lib.SDE_TOWER_F16X3,
-                    "f16x3w": _lib.SDE_TOWER_F16X3 | _lib.SDE_TOWER_WINOGRAD}
+                    "f16x3w": _lib.SDE_TOWER_F16X3 | _lib.SDE_TOWER_WINOGRAD,
+                    "f16x3m32": _lib.SDE_TOWER_F16X3 | _lib.SDE_TOWER_MFMA32}
 
 
 def _split_ptrs(split, shape):

@@ -175,11 +175,11 @@ class DisparityShardedMatcher:
         ops.preprocess_u8_batch(m.img_u82, L, out=m.img_pad2, stats=m.stats2)
         if self.band_pad is not None:
             for _stage, words in self.band_steps():
-                if m.tower_precision in ("f16x3", "f16x3w"):
+                if m.tower_precision in ("f16x3", "f16x3w", "f16x3m32"):
                     allreduce_max_(words, self.group)
             if self.band_out is not self.band:
                 self.band[:, :self.r1 - self.r0].copy_(self.band_out)
-        elif m.tower_precision in ("f16x3", "f16x3w"):
+        elif m.tower_precision in ("f16x3", "f16x3w", "f16x3m32"):
             # an empty band still joins every bound all-reduce (same count as the other ranks)
             words = torch.zeros((2, 64), dtype=torch.float32, device=m.device)
             for _ in range(L - 1):
@@ -295,10 +295,10 @@ class RowBandMatcher:
             b = self.band
             b.img_pad2.copy_(f.img_pad2[:, self.r0:self.r1 + 2 * L])
             for _stage, words in tower_steps(b.img_pad2, b.packed, L, b.feat2, b.ws, b.tower_precision, b.nf):
-                if b.tower_precision in ("f16x3", "f16x3w"):
+                if b.tower_precision in ("f16x3", "f16x3w", "f16x3m32"):
                     allreduce_max_(words, self.group)
             b.split_valid = False
-        elif f.tower_precision in ("f16x3", "f16x3w"):
+        elif f.tower_precision in ("f16x3", "f16x3w", "f16x3m32"):
             words = torch.zeros((2, 64), dtype=torch.float32, device=f.device)
             for _ in range(L - 1):
                 allreduce_max_(words, self.group)

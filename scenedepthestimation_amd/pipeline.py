@@ -42,13 +42,13 @@ def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3"
     need = ops.tower_batch_workspace_bytes(H, W, N, L, nf)
     if ws.numel() < need:
         raise ValueError("tower workspace too small")
-    cbl = precision in ("bf16x6", "f16x3", "f16x3w")
+    cbl = precision in ("bf16x6", "f16x3", "f16x3w", "f16x3m32")
     h2, w2 = H + 2 * (L - 2), W + 2 * (L - 2)
     act = h2 * w2 * nf if L > 2 else 0
     wsf = ws[: 2 * N * act * 4 + N * AMAX_WORDS * 4].view(torch.float32)
     bufs = [wsf[: N * act], wsf[N * act: 2 * N * act]]
     words = wsf[2 * N * act:].view(N, AMAX_WORDS)
-    f16 = precision in ("f16x3", "f16x3w")
+    f16 = precision in ("f16x3", "f16x3w", "f16x3m32")
     if f16:
         words.zero_()
         ops.absmax_batch(img_pad, words)

@@ -156,7 +156,8 @@ def test_argument_validation_without_gpu():
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 29960, 256, 14, 0, N, 0, N) == ERR              # just past
     assert lib.sde_cbca_pair(1, 2, 3, 4, 5, 6, 2, 29959, 256, 14, 0, N, 0, N) == 0                # just inside
     assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 2, 13108, 256, 20, 0, N, 0, N) == ERR                   # R = 31
-    assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 2, 13107, 256, 20, 0, N, 0, N) == 0
+    # accepted by the argument checks (iters 0 still writes the shear: no GPU here, so the launch fails)
+    assert lib.sde_cbca_lr(1, 2, 3, 4, 5, 2, 13107, 256, 20, 0, N, 0, N) != ERR
     assert lib.sde_lrc_fill(1, 2, 4, 65535, 3, N) == ERR                                          # 16-bit columns
     assert lib.sde_lrc_fill(1, 2, 65535, 4, 3, N) == ERR                                          # 16-bit rows
 

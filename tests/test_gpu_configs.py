@@ -270,7 +270,7 @@ def _band_features(m, world, precision):
     return full
 
 
-@pytest.mark.parametrize("precision", ["f16x3", "bf16x6", "fp32", "f16x3w"])
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x6", "fp32", "f16x3w", "f16x3m32"])
 @pytest.mark.parametrize("H,W,world", [(150, 300, 3), (97, 64, 8), (40, 70, 2)])
 def test_row_band_tower_bit_identical(gpu, precision, H, W, world):
     """Config 5's sharded tower: bands with all-reduced bound words == the full-image tower."""

@@ -169,7 +169,7 @@ def test_generic_channel_counts(gpu, golden, golden_cases):
 # ----------------------------------------------------------------------------
 # tower
 # ----------------------------------------------------------------------------
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w", "f16x3m32"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 20, 37), (5, 41, 70), (3, 17, 33), (2, 9, 40), (1, 6, 7)])
 def test_tower_vs_oracle(gpu, oracle, nlayers, H, W, precision):
     from scenedepthestimation_amd import mc_cnn, ops
@@ -197,14 +197,14 @@ def test_tower_precision_report(gpu, oracle):
     ref = oracle.tower_forward(img, hw, hb)
     packed = dev(ops.pack_tower_weights(hw, hb))
     errs = {}
-    for prec in ("fp32", "bf16x6", "f16x3", "f16x3w"):
+    for prec in ("fp32", "bf16x6", "f16x3", "f16x3w", "f16x3m32"):
         out = host(ops.tower_forward(dev(img), packed, L, precision=prec))
         errs[prec] = float(np.abs(out - ref).max())
     print("tower max abs err vs fp64:", errs)
     assert all(e < 1e-5 for e in errs.values()), errs
 
 
-@pytest.mark.parametrize("precision", ["f16x3", "f16x3w"])
+@pytest.mark.parametrize("precision", ["f16x3", "f16x3w", "f16x3m32"])
 @pytest.mark.parametrize("scale", [1e-6, 1e-3, 1e3, 1e12])
 def test_tower_f16x3_dynamic_range(gpu, oracle, scale, precision):
     """f16x3 scales operands by powers of two from device bound words: an image and weights far
@@ -228,7 +228,7 @@ def test_tower_f16x3_dynamic_range(gpu, oracle, scale, precision):
     assert err < 1e-5
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "f16x3w"])
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "f16x3w", "f16x3m32"])
 @pytest.mark.parametrize("nlayers,H,W", [(5, 700, 530), (3, 300, 1100), (2, 530, 517)])
 def test_tower_bf16x6_large_vs_fp32(gpu, nlayers, H, W, precision):
     """Sizes with more output tiles than CUs (the persistent bf16x6 kernel's tile loop, partial
@@ -258,7 +258,7 @@ def test_tower_layer_api_matches_forward(gpu):
     img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
     img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
     for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True), ("f16x3", False), ("f16x3", True),
-                      ("f16x3w", False), ("f16x3w", True)):
+                      ("f16x3w", False), ("f16x3w", True), ("f16x3m32", False), ("f16x3m32", True)):
         full = ops.tower_forward(img, packed, L, precision=prec)
         x = img
         words = torch.zeros(L, device="cuda")          # f16x3 bound words, as tower_forward keeps them
@@ -786,7 +786,7 @@ def test_feature_split_and_tower_emission(gpu, oracle):
     img[L:-L, L:-L] = rng.standard_normal((H, W)).astype(np.float32)
     w = mc_cnn.synthetic_weights(L)
     packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(w, L)))
-    for prec in ("fp32", "bf16x6"):
+    for prec in ("fp32", "bf16x6", "f16x3", "f16x3m32"):
         emitted = ops.new_split(H, W, "cuda")
         feat = ops.tower_forward(dev(img), packed, L, precision=prec, split=emitted)
         again = ops.feature_split(feat)
@@ -835,7 +835,7 @@ def test_absmax(gpu, off, n):
     assert float(word.cpu()[0]) == want
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "f16x3", "f16x3w", "f16x3m32"])
 @pytest.mark.parametrize("nlayers,H,W,N", [(5, 150, 300, 2), (3, 70, 45, 3), (2, 33, 90, 2), (1, 9, 12, 2),
                                            (5, 40, 33, 1)])
 def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
