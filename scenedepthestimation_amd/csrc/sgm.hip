@@ -1247,6 +1247,18 @@ static int sgm_pair(const float *cv_l, const float *pen_l, float *S_l, float *di
                                          dir == 0 && fold_du,
                                          wta && dir == 7);
         if (s != SDE_OK) return s;
+#ifdef SGM_GAP
+        // probe builds (tools/sgm_gap_probe.py): what sits between two passes of the pair
+        if (dir < 7) {
+            if (SGM_GAP == 1) (void)hipStreamSynchronize(st);
+            if (SGM_GAP == 2 || SGM_GAP == 3) {
+                static hipEvent_t ev = nullptr;
+                if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+                if (SGM_GAP == 2) (void)hipEventRecordWithFlags(ev, st, hipEventReleaseToSystem);
+                else (void)hipEventRecord(ev, st);
+            }
+        }
+#endif
     }
     return launch_status();
 }

@@ -40,6 +40,14 @@ constexpr int H16_HT = 18;                                // half-taps per c-blo
 constexpr int H16_RD = 3;                                 // B ring depth (fragments read RD-1 steps ahead)
 static_assert(H16_PLANE >= XP_NPIX * 16 && H16_PLANE % 256 == 0, "plane size / bank alignment");
 static_assert(H16_SMEM <= 163840, "LDS");
+// Timing-only diagnostic builds (tools/build_file_variant.sh tower.hip NAME -DH16_DIAG=n; wrong results):
+// 1 = no epilogue stores, 2 = stagers skip their loads and splits, 4 = MFMA waves reuse one A fragment
+// set (no A loads in the loop), 8 = wave 0 of each workgroup writes its (s_memtime, s_memrealtime) deltas
+// over the kernel as two floats to out[2 * blockIdx.x ..] at the end (in-kernel clock, tools/tower_variants.py).
+// 0 (the product) = everything.
+#ifndef H16_DIAG
+#define H16_DIAG 0
+#endif
 
 // Split 4 channels (chunk u & 3 of 16-channel half h of the 32-channel c-block) of pixel u >> 2,
 // scaled by s, into the stage's (part, quarter) planes.
@@ -97,6 +105,12 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
         }
     };
     float4 ra[XP_UPT], rb[XP_UPT];
+    if (H16_DIAG & 2) {
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < nsteps; i++) __syncthreads();
+        return;
+    }
     load(ra, 0);
     load(rb, 1);
     store(ra, 0);
@@ -166,7 +180,7 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A &a, H16A (&a
     for (int k = 0; k < H16_RD - 1; k++) ring[k] = h16_bfrag(sb, k);
 #pragma unroll
     for (int s = 0; s < H16_HT; s++) {
-        if (s > 0) {
+        if (s > 0 && !(H16_DIAG & 4)) {
             a = an[0];
             an[0] = an[1];
             an[1] = s + 2 < H16_HT ? h16_afrag(wf, cb, s + 2, aoff) : h16_afrag(wf, ncb, s + 2 - H16_HT, aoff);
@@ -187,9 +201,11 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A &a, H16A (&a
             if (b + H16_RD - 1 < NB) ring[(b + H16_RD - 1) % H16_RD] = h16_bfrag(sb, b + H16_RD - 1);
         }
     }
-    a = an[0];
-    an[0] = an[1];
-    an[1] = h16_afrag(wf, ncb, 2, aoff);
+    if (!(H16_DIAG & 4)) {
+        a = an[0];
+        an[0] = an[1];
+        an[1] = h16_afrag(wf, ncb, 2, aoff);
+    }
 }
 
 // Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
@@ -238,7 +254,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                             amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
                             amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
                         }
-                        xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
+                        if (!(H16_DIAG & 1)) xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
                                so);
                     }
                     if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
@@ -360,6 +376,11 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
     H16A a = h16_afrag(wf, 0, 0, aoff), an[2] = {h16_afrag(wf, 0, 1, aoff), h16_afrag(wf, 0, 2, aoff)};
     __syncthreads();
+    uint64_t clk0 = 0, rt0 = 0;
+    if (H16_DIAG & 8) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
 
     int sc_img = -1;
     float sc_u = 1.0f;
@@ -389,6 +410,11 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         }
     }
     if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+    if ((H16_DIAG & 8) && wave == 0 && lane == 0) {
+        const uint64_t c = __builtin_amdgcn_s_memtime() - clk0, r = __builtin_amdgcn_s_memrealtime() - rt0;
+        out[2 * blockIdx.x] = (float)c;
+        out[2 * blockIdx.x + 1] = (float)r;
+    }
 }
 
 }  // namespace sde

@@ -51,7 +51,7 @@ res = {}
 for rnd in range(3):
     for name, lib in libs:
         s = torch.cuda.current_stream().cuda_stream
-        for prec, flag in (("f16x3", 8), ("f16x3 winograd", 8 | 16)):
+        for prec, flag in (("f16x3", 8), ("f16x3 m32", 8 | 32)):
             def run():
                 rc = lib.sde_tower_layer_scaled(x.data_ptr(), hin, win, packed.data_ptr(), L, 64, 3, y.data_ptr(),
                                                 flag | 2 | 4, None, None, None, words.data_ptr(),
