@@ -67,6 +67,17 @@ __device__ __forceinline__ void h16_put(char *sb, int h, int u, float4 v, float 
     *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, p1);
 }
 
+// Stage unit (pixel << 2 | 4-channel chunk) of stager thread st at iteration i: a wave's lanes take 16
+// consecutive pixels x the 4 chunks (chunk = lane >> 4), so each 32-lane half of a ds_write_b64 fills one
+// quarter plane's 256 contiguous bytes (the planes are 256-B aligned: lane-contiguous units would put
+// both quarters of a pixel in one bank set), and the wave's loads still cover 1 KB of pixels contiguously.
+__device__ __forceinline__ int h16_unit(int st, int i)
+{
+    const int px = (i * (XP_STAGERS / 64) + (st >> 6)) * 16 + (st & 15);
+    return px * 4 + ((st >> 4) & 3);
+}
+static_assert(XP_UPT * XP_STAGERS / 4 >= XP_NPIX, "the stager units cover the stage's pixels");
+
 // Stager waves: half-steps k = (tile, 16-channel block cb16 = k % 4) in the MFMA waves' order; half-steps
 // 2i, 2i+1 make c-block step i (stage i & 1).  Two register sets of one half-step each are loaded
 // one c-block step ahead of their store.  One barrier per c-block step, like the MFMA waves.
@@ -85,7 +96,7 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
         const float *src = in + img * bt.in_stride;
 #pragma unroll
         for (int i = 0; i < XP_UPT; i++) {
-            const int u = st + i * XP_STAGERS;
+            const int u = h16_unit(st, i);
             v[i] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb16, u) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
@@ -100,7 +111,7 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
         char *sb = hsm + ((k >> 1) & 1) * H16_STAGE;
 #pragma unroll
         for (int i = 0; i < XP_UPT; i++) {
-            const int u = st + i * XP_STAGERS;
+            const int u = h16_unit(st, i);
             if (u < XP_UNITS) h16_put(sb, k & 1, u, v[i], s);
         }
     };
