@@ -125,6 +125,16 @@ __device__ __forceinline__ double cb_recip(uint32_t c)
     return __builtin_fma(r, e, r);
 }
 
+// Chain arithmetic: fp64 (definition v2).  CBCA_P32 builds (timing probes, tools/build_file_variant.sh) run the
+// chains, rings and the mean's reciprocal in fp32 -- different results, half the ring LDS.
+#ifdef CBCA_P32
+typedef float cb_p;
+typedef float cb_r;
+#else
+typedef double cb_p;
+typedef double cb_r;
+#endif
+
 struct CbcaArgs {
     const float *src;
     float *dst;
@@ -156,7 +166,7 @@ __device__ __forceinline__ uint32_t opq_v(uint32_t v)
 // SEL: some lane's chain starts inside the walk (d > fs: early segments); otherwise every front
 // position is on every lane's chain and the per-step select goes
 template <int R, bool SEL>
-__device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int k, double *__restrict__ sP)
+__device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int k, cb_p *__restrict__ sP)
 {
     constexpr int RS = 2 * R + 2, PF = RS;
     const int lane = threadIdx.x & 63;
@@ -197,7 +207,7 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
     for (int j = 0; j < PF; j++)
         cr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)(D4 * (uint32_t)min(fs + j, W - 1)),
                                                                                CBCA_NT & 1 ? 2 : 0));
-    double P = 0.0;
+    cb_p P = 0.0;
     sP[(RS - 1) * 64 + lane] = 0.0;               // P(fs - 1) = 0: read before position fs + RS - 1 lands
     // per-lane store offset of output t (4d + 4tD), advanced every step
     uint32_t vst = 4u * (uint32_t)d + D4 * (uint32_t)(fs - R - 1);
@@ -213,11 +223,11 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
         X = (uint32_t)__builtin_amdgcn_update_dpp((int)nb, (int)X, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- nb
         const int hl = min(a & 255u, X & 255u), hr = min((a >> 8) & 255u, (X >> 8) & 255u);
         const uint32_t ib = ring_slot<RS>(j - R - 1 + hr), ia = ring_slot<RS>(j - R - 2 - hl);
-        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        const cb_p pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
         __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front: the chain of this lane starts at max(t0 - M, d) >= fs
         const float cv = cr[slot];
-        P += (!SEL || f >= d) ? (double)cv : 0.0;
+        P += (!SEL || f >= d) ? (cb_p)cv : (cb_p)0.0;
         sP[j * 64 + lane] = P;
         const uint32_t so = clamp ? D4 * (uint32_t)min(f + PF, W - 1) : sld;
         cr[slot] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, dl4, (int)so, CBCA_NT & 1 ? 2 : 0));
@@ -272,7 +282,7 @@ __device__ __forceinline__ void cbca_h_item(const CbcaArgs &A, int y, int c, int
 template <int R>
 __global__ __launch_bounds__(64, 3) void cbca_h_kernel(const CbcaArgs A)
 {
-    __shared__ double sP[(2 * R + 2) * 64];
+    __shared__ cb_p sP[(2 * R + 2) * 64];
     for (int64_t it = blockIdx.x; it < A.nitems; it += gridDim.x) {
         const int k = (int)(it / A.nper);
         const int64_t r = it - (int64_t)k * A.nper;
@@ -300,8 +310,8 @@ template <int R> struct CbV {
 // of consecutive columns, so each row step reads whole pixels side by side.
 // ---------------------------------------------------------------------------------------------
 template <int R>
-__device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, double *__restrict__ sP,
-                                            uint16_t *__restrict__ sN, const double *__restrict__ tab)
+__device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int k, cb_p *__restrict__ sP,
+                                            uint16_t *__restrict__ sN, const cb_r *__restrict__ tab)
 {
     constexpr int RS = 2 * R + 2, PF = RS, U = R + 1;
     static_assert(RS % U == 0, "ring sizes");
@@ -349,7 +359,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
     }
 #pragma unroll
     for (int j = 0; j < U; j++) sup[j] = 0u;
-    double P = 0.0;
+    cb_p P = 0.0;
     uint32_t N = 0;
     sP[(RS - 1) * 64 + lane] = 0.0;               // Q(fs - 1) = 0, N(fs - 1) = 0
     // count ring: lane l's u16 sits at (l % 32) * 2 + l / 32 of its slot row, so a 32-lane half
@@ -378,7 +388,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         }
         const int vu = (int)vu_u, vd = (int)vd_u;
         const uint32_t ib = ring_slot<RS>(j - R - 1 + vd), ia = ring_slot<RS>(j - R - 2 - vu);
-        const double pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
+        const cb_p pb = sP[ib * 64 + lane], pa = sP[ia * 64 + lane];
         const uint16_t nb = sN[ib * 64 + ln], na = sN[ia * 64 + ln];
         __builtin_amdgcn_sched_barrier(0);   // (the reads' uses stay below the front's work)
         // front f: chain (rows >= fc), count contribution and vertical support
@@ -392,7 +402,7 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         const uint32_t m13 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a13),
                                                                                     __builtin_bit_cast(u16x2, b13)));
         const bool on = !pre || f >= fc;
-        P += on ? (double)cr[slot] : 0.0;
+        P += on ? (cb_p)cr[slot] : (cb_p)0.0;
         N += on ? ((m02 + m13) & 0xFFFFu) + 1u : 0u;
         sP[j * 64 + lane] = P;
         sN[j * 64 + ln] = (uint16_t)N;
@@ -403,10 +413,10 @@ __device__ __forceinline__ void cbca_v_item(const CbcaArgs &A, int x, int c, int
         sld = opq_s(sld + rowv);
         __builtin_amdgcn_sched_barrier(0);
         // the output (row t = f - R - 1: soffset j rows on the block's store descriptor)
-        const double num = pb - pa;
+        const cb_p num = pb - pa;
         const uint32_t cnt = (uint16_t)(nb - na);
         // (an invalid lane's count may be anything: clamped into the table)
-        const double rcp = CbV<R>::TAB ? tab[min(cnt, (uint32_t)CbV<R>::NT - 1)] : cb_recip(cnt);
+        const cb_r rcp = CbV<R>::TAB ? tab[min(cnt, (uint32_t)CbV<R>::NT - 1)] : (cb_r)cb_recip(cnt);
         const float out = (float)(num * rcp);
         const uint32_t vo = (lane_ok && t >= t0) ? 4u * (uint32_t)d : CB_OOB;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out), rd, vo, (int)sst, CBCA_NT & 2 ? 2 : 0);
@@ -457,12 +467,12 @@ template <int R>
 __global__ __launch_bounds__(64 * CbV<R>::WPB, 2) void cbca_v_kernel(const CbcaArgs A)
 {
     constexpr int WPB = CbV<R>::WPB;
-    __shared__ double sP[WPB][(2 * R + 2) * 64];
+    __shared__ cb_p sP[WPB][(2 * R + 2) * 64];
     __shared__ uint16_t sN[WPB][(2 * R + 2) * 64];
-    __shared__ double tab[CbV<R>::NT];
+    __shared__ cb_r tab[CbV<R>::NT];
     const int wave = WPB > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
     if (CbV<R>::TAB) {
-        for (int c = threadIdx.x; c < CbV<R>::NT; c += 64 * WPB) tab[c] = cb_recip((uint32_t)max(c, 1));
+        for (int c = threadIdx.x; c < CbV<R>::NT; c += 64 * WPB) tab[c] = (cb_r)cb_recip((uint32_t)max(c, 1));
         __syncthreads();
     }
     for (int64_t it = (int64_t)blockIdx.x * WPB + wave; it < A.nitems; it += (int64_t)gridDim.x * WPB) {
