@@ -1252,10 +1252,11 @@ static int sgm_pair(const float *cv_l, const float *pen_l, float *S_l, float *di
         if (dir < 7) {
             if (SGM_GAP == 1) (void)hipStreamSynchronize(st);
             if (SGM_GAP == 2 || SGM_GAP == 3) {
+                // 2: an event created with a system-scope release (L2 written back at the record)
                 static hipEvent_t ev = nullptr;
-                if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-                if (SGM_GAP == 2) (void)hipEventRecordWithFlags(ev, st, hipEventReleaseToSystem);
-                else (void)hipEventRecord(ev, st);
+                if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming |
+                                                                 (SGM_GAP == 2 ? hipEventReleaseToSystem : 0));
+                (void)hipEventRecord(ev, st);
             }
         }
 #endif

@@ -49,11 +49,10 @@ static_assert(H16_SMEM <= 163840, "LDS");
 #define H16_DIAG 0
 #endif
 
-// Split 4 channels (chunk u & 3 of 16-channel half h of the 32-channel c-block) of pixel u >> 2,
-// scaled by s, into the stage's (part, quarter) planes.
-__device__ __forceinline__ void h16_put(char *sb, int h, int u, float4 v, float s)
+// Split 4 channels, scaled by s, into the stage's (part, quarter) planes at dst (the unit's byte offset
+// in the stage, see h16_stager_loop).
+__device__ __forceinline__ void h16_put(char *dst, float4 v, float s)
 {
-    const int px = u >> 2, chunk = u & 3;
     f16x4 p0, p1;
     const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
 #pragma unroll
@@ -62,7 +61,6 @@ __device__ __forceinline__ void h16_put(char *sb, int h, int u, float4 v, float 
         p0[e] = hh;
         p1[e] = (_Float16)(xs[e] - (float)hh);
     }
-    char *dst = sb + (2 * h + (chunk >> 1)) * H16_PLANE + px * 16 + (chunk & 1) * 8;
     *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
     *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, p1);
 }
@@ -81,6 +79,9 @@ static_assert(XP_UPT * XP_STAGERS / 4 >= XP_NPIX, "the stager units cover the st
 // Stager waves: half-steps k = (tile, 16-channel block cb16 = k % 4) in the MFMA waves' order; half-steps
 // 2i, 2i+1 make c-block step i (stage i & 1).  Two register sets of one half-step each are loaded
 // one c-block step ahead of their store.  One barrier per c-block step, like the MFMA waves.
+// A unit's global and LDS offsets are tile-invariant: computed once; per half-step a wave-uniform
+// buffer descriptor at the tile's origin (loads outside the input take an offset past the records
+// and return the zero padding), and interior tiles skip the bound tests.
 template <bool IN_CB>
 __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restrict__ in, int Hin, int Win,
                                                 const XpBatch &bt, int st, const float *__restrict__ in_amax,
@@ -89,15 +90,35 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
     const int tile0 = blockIdx.x, gstride = gridDim.x;
     const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * H16_NCB;
     const int nh = 2 * nsteps;
+    uint32_t uoff[XP_UPT], uyx[XP_UPT], ulds[XP_UPT];
+#pragma unroll
+    for (int i = 0; i < XP_UPT; i++) {
+        const int u = h16_unit(st, i), px = u >> 2, chunk = u & 3;
+        const int iy = px / XP_IX, ix = px - iy * XP_IX;
+        const bool ok = u < XP_UNITS;
+        uoff[i] = ok ? (uint32_t)((iy * Win + ix) * (IN_CB ? 64 : 256) + 16 * chunk) : XP_OOB;
+        uyx[i] = ok ? (uint32_t)(iy << 16 | ix) : 0xFFFF0000u;
+        ulds[i] = ok ? (uint32_t)((chunk >> 1) * H16_PLANE + px * 16 + (chunk & 1) * 8) : 0u;
+    }
     auto load = [&](float4 (&v)[XP_UPT], int k) {
         const int t = tile0 + (k >> 2) * gstride, cb16 = k & 3;
         int img, ty0, tx0;
         xp_tile(bt, t, img, ty0, tx0);
         const float *src = in + img * bt.in_stride;
+        const __amdgpu_buffer_rsrc_t rs =
+            xp_rsrc(IN_CB ? src + (((size_t)cb16 * Hin + ty0) * Win + tx0) * 16
+                          : src + ((size_t)ty0 * Win + tx0) * 64 + cb16 * 16);
+        const int ly = Hin - ty0, lx = Win - tx0;
+        if (ly >= XP_IY && lx >= XP_IX) {   // wave-uniform: the tile's input window is inside the input
 #pragma unroll
-        for (int i = 0; i < XP_UPT; i++) {
-            const int u = h16_unit(st, i);
-            v[i] = u < XP_UNITS ? xp_load<IN_CB>(src, Hin, Win, ty0, tx0, cb16, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int i = 0; i < XP_UPT; i++)
+                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, uoff[i], 0, 0));
+        } else {
+#pragma unroll
+            for (int i = 0; i < XP_UPT; i++) {
+                const bool ok = (int)(uyx[i] >> 16) < ly && (int)(uyx[i] & 0xFFFFu) < lx;
+                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? uoff[i] : XP_OOB, 0, 0));
+            }
         }
     };
     int sc_img = -1;
@@ -108,12 +129,11 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
             xp_scales(false, in_amax + im * bt.amax_stride, hdr, s, unscale);
             sc_img = im;
         }
-        char *sb = hsm + ((k >> 1) & 1) * H16_STAGE;
+        // half h = k & 1 of the c-block: quarter planes 2h, 2h + 1
+        char *sb = hsm + ((k >> 1) & 1) * H16_STAGE + (k & 1) * 2 * H16_PLANE;
 #pragma unroll
-        for (int i = 0; i < XP_UPT; i++) {
-            const int u = h16_unit(st, i);
-            if (u < XP_UNITS) h16_put(sb, k & 1, u, v[i], s);
-        }
+        for (int i = 0; i < XP_UPT; i++)
+            if (h16_unit(st, i) < XP_UNITS) h16_put(sb + ulds[i], v[i], s);
     };
     float4 ra[XP_UPT], rb[XP_UPT];
     if (H16_DIAG & 2) {
@@ -141,21 +161,26 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
     }
 }
 
-// A fragments of one half-tap (tap s >> 1, quarters 2 (s & 1) + qq) of 32-channel c-block cb:
-// [part][qq].  aoff = the lane's offset in the F16 blob's A-fragment order (uint4 units, qq = 0).
+// A fragments of one half-tap (tap s >> 1, quarters 2 (s & 1) + qq) of 32-channel c-block cb: [part][qq],
+// by buffer loads: ra = the layer's F16 A-fragment blob, voff = the lane's byte offset in its
+// [mtile][cblock16][tap][part][lane][8] order, cbo = cb's byte offset (wave-uniform); the rest of the
+// offset is a compile-time constant (no per-load VALU address arithmetic).
 struct H16A {
     f16x8 f[2][2];
 };
+constexpr int H16_A_CB = 2 * 9 * 2 * 64 * 16;   // bytes per 32-channel c-block of one M-tile
 
-__device__ __forceinline__ H16A h16_afrag(const uint4 *__restrict__ wf, int cb, int s, int aoff)
+__device__ __forceinline__ H16A h16_afrag(__amdgpu_buffer_rsrc_t ra, uint32_t voff, int cbo, int s)
 {
     const int tap = s >> 1, hf = s & 1;
     H16A a;
 #pragma unroll
     for (int p = 0; p < 2; p++)
 #pragma unroll
-        for (int qq = 0; qq < 2; qq++)
-            a.f[p][qq] = __builtin_bit_cast(f16x8, wf[((((hf * XP_NCB + 2 * cb) * 9 + tap) * 2 + p) * 64) + aoff + 16 * qq]);
+        for (int qq = 0; qq < 2; qq++) {
+            const int k = (((hf * XP_NCB * 9 + tap) * 2 + p) * 64 + 16 * qq) * 16;
+            a.f[p][qq] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, cbo + k, 0));
+        }
     return a;
 }
 
@@ -181,21 +206,23 @@ __device__ __forceinline__ floatx4 mfma16(f16x8 a, f16x8 b, floatx4 c)
 }
 
 // One 32-channel c-block for one MFMA wave: 18 half-taps x 8 (row, half) steps, 6 MFMAs each.
-// acc[(r * 2 + ph) * 4 + q].  a = A(cb, 0), an[k] = A(cb, 1 + k) on entry; A(ncb, 0..) on exit.
-__device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A &a, H16A (&an)[2], const uint4 *__restrict__ wf,
-                                           int cb, int ncb, int aoff, const char *sb)
+// acc[(r * 2 + ph) * 4 + q].  A ring of three half-taps with static slots (18 = 6 x 3: every c-block
+// starts in the same phase): on entry abuf[0] = A(cb, 0) and abuf[1] = A(cb, 1) are requested; half-tap s
+// requests A(s + 2) into the slot A(s - 1) left; on exit abuf[0..1] = A(ncb, 0..1).
+__device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[3], __amdgpu_buffer_rsrc_t ra,
+                                           uint32_t avoff, int cb, int ncb, const char *sb)
 {
     constexpr int NB = H16_HT * 8;
+    static_assert(H16_HT % 3 == 0, "A ring phase");
     H16B ring[H16_RD];
 #pragma unroll
     for (int k = 0; k < H16_RD - 1; k++) ring[k] = h16_bfrag(sb, k);
 #pragma unroll
     for (int s = 0; s < H16_HT; s++) {
-        if (s > 0 && !(H16_DIAG & 4)) {
-            a = an[0];
-            an[0] = an[1];
-            an[1] = s + 2 < H16_HT ? h16_afrag(wf, cb, s + 2, aoff) : h16_afrag(wf, ncb, s + 2 - H16_HT, aoff);
-        }
+        if (!(H16_DIAG & 4))
+            abuf[(s + 2) % 3] = s + 2 < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, s + 2)
+                                               : h16_afrag(ra, avoff, ncb * H16_A_CB, s + 2 - H16_HT);
+        const H16A &a = abuf[(H16_DIAG & 4) ? 0 : s % 3];
         const int hf = s & 1;
 #pragma unroll
         for (int rp = 0; rp < 8; rp++) {
@@ -211,11 +238,6 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A &a, H16A (&a
             }
             if (b + H16_RD - 1 < NB) ring[(b + H16_RD - 1) % H16_RD] = h16_bfrag(sb, b + H16_RD - 1);
         }
-    }
-    if (!(H16_DIAG & 4)) {
-        a = an[0];
-        an[0] = an[1];
-        an[1] = h16_afrag(wf, ncb, 2, aoff);
     }
 }
 
@@ -380,12 +402,14 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     float *lbias = reinterpret_cast<float *>(hsm + H16_BIAS_OFF);
     if (wave == 0) lbias[lane] = wkblob[lane];   // published by the first barrier below
     const float4 *lbias4 = reinterpret_cast<const float4 *>(lbias);
-    const uint4 *wf = reinterpret_cast<const uint4 *>(wkblob + LK_F16);
-    // the lane's A-fragment offset: cb16 = 2 cb + (lane >> 5), channel half (lane >> 4) & 1, n & 15
-    const int aoff = (lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15);
+    const __amdgpu_buffer_rsrc_t ra = xp_rsrc(wkblob + LK_F16);
+    // the lane's A-fragment byte offset: cb16 = 2 cb + (lane >> 5), channel half (lane >> 4) & 1, n & 15
+    const uint32_t avoff = (uint32_t)((lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15)) * 16u;
     // the lane's B base: plane quarter lane >> 4, pixel (4g, lane & 15) of the input tile
     const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
-    H16A a = h16_afrag(wf, 0, 0, aoff), an[2] = {h16_afrag(wf, 0, 1, aoff), h16_afrag(wf, 0, 2, aoff)};
+    H16A abuf[3];
+    abuf[0] = h16_afrag(ra, avoff, 0, 0);
+    abuf[1] = h16_afrag(ra, avoff, 0, 1);
     __syncthreads();
     uint64_t clk0 = 0, rt0 = 0;
     if (H16_DIAG & 8) {
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         for (int i = 0; i < 32; i++) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
         for (int cb = 0; cb < H16_NCB; cb++) {
-            h16_cblock(acc, a, an, wf, cb, cb ^ 1, aoff, hsm + cur * H16_STAGE + bbase);
+            h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             if (cb == H16_NCB - 1) {
                 if (img != sc_img) {
                     float s_unused;

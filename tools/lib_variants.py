@@ -27,8 +27,9 @@ pen = [ops.sgm_penalties(i) for i in imgu8]
 disp = [torch.empty((H, W), device="cuda") for _ in range(2)]
 P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 here = os.path.dirname(os.path.abspath(__file__))
-sos = [_lib.LIB] + sorted(f for f in glob.glob(os.path.join(here, "_var", "libsde_*.so"))
-                          if not os.path.basename(f).startswith("libsde_sgm_"))   # (sgm_variants.py's)
+# SDE_VARIANTS: a glob of the variant libraries to time (default: all but sgm_variants.py's)
+sos = [_lib.LIB] + sorted(f for f in glob.glob(os.path.join(here, "_var", os.environ.get("SDE_VARIANTS", "libsde_*.so")))
+                          if not os.path.basename(f).startswith("libsde_sgm_"))
 libs = []
 for so in sos:
     lib = ctypes.CDLL(so)
