@@ -345,6 +345,8 @@ def gpu_path_stages(m: StereoMatcher, prefix: str = ""):
     path_ms = _events_ms(lambda: m.sgm_path(post=True))
     tower_ms = _events_ms(lambda: m.features())
     out[prefix + "gpu_path_ms"] = path_ms
+    # the SGM volumes' placement draws (pipeline.StereoMatcher._place_sgm_volumes): pair ms per draw
+    out[prefix + "sgm_placement_draws_ms"] = m.sgm_placement_ms
     out[prefix + "ms_per_pair_tower_plus_gpu_path"] = tower_ms + path_ms
     kern = {}
     # cvlr3_kernel: reads both feature maps once, writes the L and R [H,W,D] volumes -- the left one only

@@ -23,6 +23,11 @@ from . import mc_cnn, ops
 
 
 AMAX_WORDS = 64   # f16x3 bound words per image in the tower workspace (TOWER_AMAX_BYTES / 4)
+# Placement draws of the four SGM volumes (StereoMatcher._place_sgm_volumes): volumes of [MIN, MAX] voxels are
+# placed by up to this many allocate-and-time draws (larger ones would hold three 4-volume sets of > 6 GB each).
+SGM_PLACEMENT_TRIALS = 8
+SGM_PLACEMENT_MIN_VOXELS = 1 << 26
+SGM_PLACEMENT_MAX_VOXELS = 1 << 29
 
 
 def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3", nf: int = 64, on_launch=None):
@@ -90,11 +95,13 @@ class StereoMatcher:
     def __init__(self, height: int, width: int, ndisp: int, weights=None, nlayers: int = 5,
                  nf: int = 64, device=None, d_range=None, sgm: bool = False, tower_precision: str = "f16x3",
                  cv_mode: str = "certified", cbca_iters: int = 0, cbca_L1: int = 14, cbca_tau: float = 0.02,
-                 emit_split: bool = False):
+                 emit_split: bool = False, sgm_placement_trials: int = SGM_PLACEMENT_TRIALS):
         self.H, self.W, self.D = int(height), int(width), int(ndisp)
         # cross-based aggregation before SGM (build-defined stage; 0 = the reference's GPU path)
         self.cbca_iters, self.cbca_L1, self.cbca_tau = int(cbca_iters), int(cbca_L1), float(cbca_tau)
         self.nlayers, self.nf = int(nlayers), int(nf)
+        self.sgm_placement_trials = int(sgm_placement_trials)
+        self.sgm_placement_ms = None     # the SGM pair time of each placement draw (_place_sgm_volumes)
         if tower_precision not in ops.TOWER_PRECISIONS:
             raise ValueError(f"tower_precision must be one of {sorted(ops.TOWER_PRECISIONS)}")
         self.tower_precision = tower_precision
@@ -199,17 +206,73 @@ class StereoMatcher:
         return self.disp
 
     # -- GPU path of disparity_compute_by_gpu ---------------------------------
+    def _place_sgm_volumes(self, pen, disp):
+        """The four [H,W,D] volumes of the GPU path (cost L/R, SGM S L/R), placed by allocate-and-time draws.
+
+        The 7-launch SGM pair moves the same bytes through any four volumes, yet on MI355X it runs in one of two
+        modes by where the allocation lands in HBM: ~5.3 or ~5.7-5.8 ms at 1024^2 x 192 (LR/RL 0.81 vs 0.95 ms
+        per launch, the diagonals 0.80 vs 0.85; the same virtual addresses can come back in either mode,
+        row strides and offsets inside one allocation do not decide it, the box's thermal / power state does not
+        either -- tools/sgm_*_probe.py).  So for large volumes each draw allocates a fresh
+        set (the previous one still held, so the draw gets other memory), times one pair on zero costs, and the
+        fastest set is kept; the draws stop once one beats the slowest seen by 6 % (both modes seen).  One-time
+        cost: ~20 ms per draw."""
+        H, W, D, dev = self.H, self.W, self.D, self.device
+
+        def new_set():
+            return [torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(4)]
+        trials = self.sgm_placement_trials if SGM_PLACEMENT_MIN_VOXELS <= H * W * D <= SGM_PLACEMENT_MAX_VOXELS else 1
+        if trials <= 1:
+            return new_set()
+        for p in pen:
+            p.zero_()
+
+        def pair_ms(v):
+            for t in v:
+                t.zero_()
+            run = lambda: ops.sgm_8path_wta_pair(v[0], pen[0], v[2], disp[0], v[1], pen[1], v[3], disp[1],  # noqa: E731
+                                                 zero_du_penalties=True)
+            run()
+            best = float("inf")
+            for _ in range(2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                run()
+                e1.record()
+                torch.cuda.synchronize(dev)
+                best = min(best, e0.elapsed_time(e1))
+            return best
+        best, best_ms, worst, prev, times = None, float("inf"), 0.0, None, []
+        for _ in range(trials):
+            cur = new_set()
+            ms = pair_ms(cur)
+            times.append(ms)
+            worst = max(worst, ms)
+            if ms < best_ms:
+                best, best_ms = cur, ms
+            prev = cur
+            torch.cuda.empty_cache()
+            if best_ms <= 0.94 * worst:
+                break
+        del prev, cur
+        torch.cuda.empty_cache()
+        self.sgm_placement_ms = times
+        return best
+
     def _alloc_sgm(self):
         H, W, D, dev = self.H, self.W, self.D, self.device
+        pen = [torch.empty((H, W, 16), dtype=torch.float32, device=dev) for _ in range(2)]
+        disp = [torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(2)]
+        cvl, cvr, sl, sr = self._place_sgm_volumes(pen, disp)
+        # the right volume starts as the GPU path's invalid fill (1.0): with aggregation on, the cost
+        # volume sweep writes the left volume only and sde_cbca_lr the right one's valid voxels, so its
+        # invalid voxels (x + d >= W) keep this fill -- the value the two-volume sweep writes there
+        cvr.fill_(1.0)
         self.sgm_bufs = dict(
-            # the right volume starts as the GPU path's invalid fill (1.0): with aggregation on, the cost
-            # volume sweep writes the left volume only and sde_cbca_lr the right one's valid voxels, so its
-            # invalid voxels (x + d >= W) keep this fill -- the value the two-volume sweep writes there
-            cv=[torch.empty((H, W, D), dtype=torch.float32, device=dev),
-                torch.full((H, W, D), 1.0, dtype=torch.float32, device=dev)],
-            pen=[torch.empty((H, W, 16), dtype=torch.float32, device=dev) for _ in range(2)],
-            S=[torch.empty((H, W, D), dtype=torch.float32, device=dev) for _ in range(2)],
-            disp=[torch.empty((H, W), dtype=torch.float32, device=dev) for _ in range(2)],
+            cv=[cvl, cvr],
+            pen=pen,
+            S=[sl, sr],
+            disp=disp,
             lrc=[torch.empty((H, W), dtype=torch.uint8, device=dev) for _ in range(2)],
             disp_a=torch.empty((H, W), dtype=torch.float32, device=dev),
             disp_b=torch.empty((H, W), dtype=torch.float32, device=dev),
