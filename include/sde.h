@@ -151,11 +151,20 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
  * products, more VALU; slower than the direct kernel at 1024^2 on MI355X -- DESIGN.md 3.2). */
 #define SDE_TOWER_WINOGRAD 16
 /* With SDE_TOWER_F16X3 only: run the 64 -> 64 layers on the v_mfma_f32_32x32x16_f16 direct kernel instead of
- * the default v_mfma_f32_16x16x32_f16 one (same arithmetic contract).  Layers whose last-layer
- * epilogue writes the split planes always take the 32x32x16 kernel. */
+ * the default v_mfma_f32_16x16x32_f16 one (same arithmetic contract). */
 #define SDE_TOWER_MFMA32 32
 #define SDE_TOWER_IN_CBLOCK 2
 #define SDE_TOWER_OUT_CBLOCK 4
+/* F16X3 split activations (sde_tower_layer_scaled / sde_tower_layer_batch; what sde_tower_forward uses
+ * between the 64->64 layers of the default f16x3 tower): OUT_SPLIT writes a layer's ReLU outputs scaled by
+ * 2^sigma and split exactly into two fp16 parts, per image 16 planes [cblk32 2][part 2][quarter 4] of
+ * [h][w][8 fp16] (256 B per pixel, as fp32 [h][w][64]), and publishes 2^sigma at out_absmax[32] (per image);
+ * IN_SPLIT reads that layout and in_absmax[32] (LDS-DMA staging, no arithmetic).  2^sigma comes from an
+ * a-priori bound of the outputs (max |b| + L1 * input bound, no fp16 overflow).  Layers >= 3 (IN) and
+ * < nlayers (OUT), a layer between them with both or neither; at most 32 layers, fewer than 2^24 input pixels; bound-word arrays of >= 33 words per
+ * image; not with the CBLOCK flag of the same side, WINOGRAD or MFMA32. */
+#define SDE_TOWER_IN_SPLIT 64
+#define SDE_TOWER_OUT_SPLIT 128
 
 /* Number of floats of the packed (device-layout) weight blob (fp32 + pre-split bf16 planes). */
 int64_t sde_tower_packed_floats(int nlayers, int nf);

@@ -29,6 +29,7 @@ SDE_TOWER_FP32, SDE_TOWER_BF16X6, SDE_TOWER_F16X3 = 0, 1, 8
 SDE_TOWER_IN_CBLOCK, SDE_TOWER_OUT_CBLOCK = 2, 4
 SDE_TOWER_WINOGRAD = 16
 SDE_TOWER_MFMA32 = 32
+SDE_TOWER_IN_SPLIT, SDE_TOWER_OUT_SPLIT = 64, 128
 SDE_CV_EXACT, SDE_CV_CERTIFIED = 0, 1
 SDE_SGM_ACCUMULATE = 1
 SDE_SGM_ZERO_DU_PENALTIES = 2

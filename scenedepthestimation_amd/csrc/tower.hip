@@ -41,11 +41,13 @@ constexpr int LK_W = 9 * NF * NF;                // one [tap][n][c] plane, eleme
 // layer k >= 2: bias f32 [64] | W f32 [tap][n][c] | bf16 parts (hi, mid, lo: W = hi+mid+lo) in A-fragment order
 // [mtile 2][cblock 4][tap 9][part 3][lane 64][8] for conv64_x6p_kernel | fp16 parts of W * 2^tau (hi, lo)
 // [mtile 2][cblock 4][tap 9][part 2][lane 64][8] for the F16 variant | F16 header {2^-tau, conv1 L1 bound,
-// max |b1|, 0} (the conv1 terms are used by layer 2, which computes conv1)
+// max |b1|, 0, L1 bound of this layer (max_n sum_{tap,c} |w|), its max |b|, 0, 0} (the conv1 terms are used
+// by layer 2, which computes conv1; the layer's own terms bound its outputs for the split activations)
 constexpr int LK_F16 = NF + LK_W + 3 * LK_W / 2;   // float offset of the fp16 parts
+constexpr int LK_HDR = 8;                           // F16 header floats
 // Winograd F(2x2,3x3) U = G g G^T (tower_wino.h): [xi 16][mtile 2][cblock 4][part 2][lane 64][8] fp16
 // after the F16 header, then its own header {2^-tau_u, 0, 0, 0}
-constexpr int LK_WINO = LK_F16 + LK_W + 4;
+constexpr int LK_WINO = LK_F16 + LK_W + LK_HDR;
 constexpr int LK_WU = 16 * NF * NF * 2;                // fp16 elements
 constexpr int LK_WHDR = LK_WINO + LK_WU / 2;
 constexpr int LK_FLOATS = LK_WHDR + 4;
@@ -482,18 +484,54 @@ __device__ __forceinline__ void xp_fill(char *sb, const float *__restrict__ in, 
     }
 }
 
+// 2^sigma for a bound: bound * 2^sigma in [2^14, 2^15); a zero, subnormal or non-finite bound gives sigma = 14
+__device__ __forceinline__ int xp_sigma(float bound)
+{
+    int e = 0;   // bound in [2^e, 2^(e+1))
+    if (bound >= 1.17549435e-38f && bound <= 3.40282347e38f) e = (int)((__float_as_uint(bound) >> 23) & 255u) - 127;
+    return min(max(14 - e, -100), 100);
+}
+
 // F16 scalings of one tile (see above): s = 2^sigma for the stagers, unscale = 2^-(tau+sigma).
 // hdr: the layer blob's F16 header {2^-tau, max_n sum_t |w1[t][n]|, max |b1|, 0}.
 __device__ __forceinline__ void xp_scales(bool first, const float *__restrict__ in_amax, const float *__restrict__ hdr,
                                           float &s, float &unscale)
 {
     const float m = *in_amax;
-    const float bound = first ? fmaf(m, hdr[1], hdr[2]) : m;
-    int e = 0;   // bound in [2^e, 2^(e+1)); a zero, subnormal or non-finite bound leaves sigma = 14
-    if (bound >= 1.17549435e-38f && bound <= 3.40282347e38f) e = (int)((__float_as_uint(bound) >> 23) & 255u) - 127;
-    const int sigma = min(max(14 - e, -100), 100);
+    const int sigma = xp_sigma(first ? fmaf(m, hdr[1], hdr[2]) : m);
     s = ldexpf(1.0f, sigma);
     unscale = ldexpf(hdr[0], -sigma);
+}
+
+// Split activations (SDE_TOWER_OUT_SPLIT / SDE_TOWER_IN_SPLIT): a layer writes its ReLU outputs already
+// scaled and split into the two fp16 parts its reader stages, so the reader's stagers copy them to LDS
+// with LDS-DMA and no arithmetic.  The writer cannot know the measured maximum of its outputs before it
+// writes them, so its 2^sigma comes from an a-priori bound: |out| <= max|b| + L1 * bound(|input|) (hdr[4],
+// hdr[5], rounded up on the host; x 1.001 covers the f16x3 error of the computed outputs) -- bound * 2^sigma
+// in [2^14, 2^15), no fp16 overflow.  The bound is looser than the measured maximum by the layer's L1 gain
+// only (the input term is the measured bound word), which costs nothing here: values far below the bound
+// lose precision only as fp16 subnormals do, an absolute error <= 2^-25 * 2^-sigma = 2^-39 of the bound.
+// The writer publishes 2^sigma at its bound word + XP_SCALE_WORD (per image); the reader's unscale is
+// 2^-tau / 2^sigma (exact).  Layout of a split activation (per image): 16 planes [cblk32 2][part 2][q 4],
+// each [h][w][8 fp16] (16 B per pixel): the same 256 B per pixel as the fp32 [h][w][64].
+constexpr int XP_SCALE_WORD = 32;
+__device__ __forceinline__ float xp_out_scale(bool first, const float *__restrict__ in_amax,
+                                              const float *__restrict__ hdr)
+{
+    const float m = *in_amax;
+    const float bin = first ? fmaf(m, hdr[1], hdr[2]) : m;
+    return ldexpf(1.0f, xp_sigma(fmaf(bin, hdr[4], hdr[5]) * 1.001f));
+}
+
+// the writer's 2^sigma into out_amax[img * stride + XP_SCALE_WORD] for every image of the launch
+// (workgroup 0, wave 0; every workgroup would compute the same value)
+__device__ __forceinline__ void xp_publish_scale(bool first, const XpBatch &bt, const float *__restrict__ in_amax,
+                                                 const float *__restrict__ hdr, float *__restrict__ out_amax)
+{
+    if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+    const int nimg = bt.ntiles / bt.tiles_img;
+    for (int im = threadIdx.x; im < nimg; im += 64)
+        out_amax[im * bt.amax_stride + XP_SCALE_WORD] = xp_out_scale(first, in_amax + im * bt.amax_stride, hdr);
 }
 
 // Stager waves' own loop (non-FIRST layers): the pipeline of (tile, c-block) steps the MFMA
@@ -654,6 +692,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t xp_rsrc(const void *base)
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)hi << 32) | lo), 0, (int)XP_NREC, 0x00020000);
 }
 
+// the same with nrec bytes of records (loads past them return zero)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xp_rsrc_n(const void *base, uint32_t nrec)
+{
+    const uintptr_t b = (uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+}
+
 __device__ __forceinline__ void xp_st4(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so)
 {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
@@ -725,6 +773,18 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
     }
 }
 
+// o * s (s = 2^sigma) split exactly into two fp16 parts: hi = fp16(o s), lo = fp16(o s - hi)
+__device__ __forceinline__ void xp_split16(float4 o, float s, f16x4 &hv, f16x4 &lv)
+{
+    const float xs[4] = {o.x * s, o.y * s, o.z * s, o.w * s};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const _Float16 hh = (_Float16)xs[e];
+        hv[e] = hh;
+        lv[e] = (_Float16)(xs[e] - (float)hh);
+    }
+}
+
 // Tile epilogue of one MFMA wave (output rows WR*g .., M-tiles mt0 ..): bias (+ReLU | L2-normalise),
 // stores, and (F16, !LAST) the running maximum of the stored outputs for the image's bound word
 // (one atomic per wave and image, xp_flush_amax).  unscale undoes the F16 power-of-two scalings.
@@ -741,14 +801,15 @@ __device__ __forceinline__ void xp_flush_amax(uint32_t &amax_run, int &amax_img,
 
 constexpr int XP_PIN = 4;   // a stored float4's registers are not rewritten before XP_PIN - 1 more stores issue
 
-template <bool LAST, bool OUT_CB, bool F16, int XP_WROWS>
+template <bool LAST, bool OUT_CB, bool F16, int XP_WROWS, bool OSPL = false>
 __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int lane, int g, int mt0, int img,
                                             int ty0, int tx0, float unscale, const float4 *lbias4,
                                             float *__restrict__ out, int Hout, int Wout, const XpBatch &bt,
                                             uint16_t *__restrict__ ohi, uint16_t *__restrict__ olo,
                                             float *__restrict__ onrm, uint32_t &amax_run, int &amax_img,
-                                            float *__restrict__ out_amax)
+                                            float *__restrict__ out_amax, float oscale = 1.0f)
 {
+    static_assert(!OSPL || (F16 && !LAST && !OUT_CB), "split outputs: F16 intermediate layers");
     constexpr int MW = 8 / XP_WROWS;
     // ---- epilogue (MFMA waves): bias (+ReLU | L2-normalise) ------------
     // lane holds pixel column j, channels m*32 + 8q + 4h + e in acc[m * XP_WROWS + r][4q + e]
@@ -784,9 +845,12 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
 #pragma unroll
             for (int qh = 0; qh < 2; qh++) {
                 const int cblk = 2 * (mt0 + m) + qh;
+                // OSPL: the hi planes of 32-channel block mt0 + m at the tile's first row (q and the part
+                // ride in the SGPR offset: plane (cblk32 * 2 + part) * 4 + q)
                 const __amdgpu_buffer_rsrc_t rs =
-                    xp_rsrc(OUT_CB ? outi + ((size_t)cblk * HW + (size_t)ty0 * Wout) * 16
-                                   : outi + (size_t)ty0 * Wout * NF);
+                    OSPL ? xp_rsrc(reinterpret_cast<char *>(outi) + (size_t)(mt0 + m) * 8 * HW * 16 + (size_t)ty0 * Wout * 16)
+                         : xp_rsrc(OUT_CB ? outi + ((size_t)cblk * HW + (size_t)ty0 * Wout) * 16
+                                          : outi + (size_t)ty0 * Wout * NF);
 #pragma unroll
                 for (int r = 0; r < XP_WROWS; r++) {
                     const floatx16 &c = acc[m * XP_WROWS + r];
@@ -802,14 +866,39 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
                             o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]), 0.f);
                         const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                         const int k = ((m * 2 + qh) * XP_WROWS + r) * 2 + ql;
-                        pin[k] = __builtin_bit_cast(u32x4, o);
-                        if (rok) {
-                            if (F16) {   // the bound before the store: nothing writes o's registers after it
+                        if (OSPL) {
+                            // scaled fp16 parts of channels 32 (mt0 + m) + 8q + 4h ..: the lane pair (h = 0, 1)
+                            // swaps halves (v_permlane32_swap) so that lane h = 0 holds the group's 8 hi parts
+                            // and h = 1 its 8 lo parts: one 16-B store each, to plane (mt0 + m) * 8 + h * 4 + q
+                            f16x4 hv, lv;
+                            xp_split16(o, oscale, hv, lv);
+                            u32x2 hw2 = __builtin_bit_cast(u32x2, hv), lw2 = __builtin_bit_cast(u32x2, lv);
+#pragma unroll
+                            for (int w = 0; w < 2; w++) {   // upper half's hi <-> lower half's lo
+                                const auto sw = __builtin_amdgcn_permlane32_swap(hw2[w], lw2[w], false, false);
+                                hw2[w] = sw[0];
+                                lw2[w] = sw[1];
+                            }
+                            const u32x4 v4 = {hw2.x, hw2.y, lw2.x, lw2.y};
+                            pin[k] = v4;
+                            if (rok) {
                                 amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
                                 amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                                const uint32_t pb = (uint32_t)HW * 16u;
+                                const uint32_t v2 = xok ? (uint32_t)(x * 16) + (uint32_t)h * 4u * pb : XP_OOB;
+                                const uint32_t s2 = (uint32_t)((row0 + r) * Wout) * 16u;
+                                __builtin_amdgcn_raw_buffer_store_b128(v4, rs, v2, s2 + q * pb, 0);
                             }
-                            // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
-                            xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
+                        } else {
+                            pin[k] = __builtin_bit_cast(u32x4, o);
+                            if (rok) {
+                                if (F16) {   // the bound before the store: nothing writes o's registers after it
+                                    amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                                    amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                                }
+                                // byte offset within the descriptor: OUT_CB 32 (q & 1); else ch * 4
+                                xp_st4(o, rs, vo + (OUT_CB ? 32u * ql : 4u * ((mt0 + m) * 32 + 8 * q)), so);
+                            }
                         }
                         if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
                     }
@@ -917,7 +1006,7 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
     }
 }
 
-template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB, bool F16>
+template <bool FIRST, bool LAST, bool IN_CB, bool OUT_CB, bool F16, bool OSPL = false>
 __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ w1blob,
                                                          const float *__restrict__ wkblob,
@@ -970,6 +1059,7 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
         xp_stager_loop<FIRST, IN_CB, F16>(xsm, in, Hin, Win, bt, st, in_amax, hdr, w1blob, win);
         return;
     }
+    if (OSPL) xp_publish_scale(FIRST, bt, in_amax, hdr, out_amax);
     float *lbias = reinterpret_cast<float *>(xsm + XP_BIAS_OFF);
     if (wave == 0) lbias[lane] = bias[lane];   // published by the first barrier below
     const float4 *lbias4 = reinterpret_cast<const float4 *>(lbias);
@@ -983,7 +1073,8 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
     __syncthreads();
 
     uint32_t amax_run = 0u;
-    int amax_img = -1;
+    int amax_img = -1, osc_img = -1;
+    float osc = 1.0f;
     int cur = 0;
     for (; tile < bt.ntiles; tile += gridDim.x) {
         int img, ty0, tx0;
@@ -1002,8 +1093,17 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
                     float s_unused;
                     scales(tile, s_unused, unscale);
                 }
-                xp_epilogue<LAST, OUT_CB, F16, XP_WROWS>(acc, lane, g, mt0, img, ty0, tx0, unscale, lbias4, out, Hout,
-                                                         Wout, bt, ohi, olo, onrm, amax_run, amax_img, out_amax);
+                float oscale = 1.0f;
+                if (OSPL) {
+                    if (img != osc_img) {
+                        osc = xp_out_scale(FIRST, in_amax + img * bt.amax_stride, hdr);
+                        osc_img = img;
+                    }
+                    oscale = osc;
+                }
+                xp_epilogue<LAST, OUT_CB, F16, XP_WROWS, OSPL>(acc, lane, g, mt0, img, ty0, tx0, unscale, lbias4, out,
+                                                               Hout, Wout, bt, ohi, olo, onrm, amax_run, amax_img,
+                                                               out_amax, oscale);
             }
             __syncthreads();
             cur ^= 1;
@@ -1015,6 +1115,10 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 }  // namespace sde
 #include "tower_wino.h"
 #include "tower_h16.h"
+#include "tower_h16q.h"
+#ifndef SDE_H16Q
+#define SDE_H16Q 1   // 0: timing builds only -- middle split layers on conv64_h16_kernel's 8-wave form
+#endif
 namespace sde {
 
 
@@ -1279,6 +1383,18 @@ SDE_EXPORT int sde_tower_pack_weights(const float *const *hwio, const float *con
         hdr[1] = l1;
         hdr[2] = bmax;
         hdr[3] = 0.0f;
+        {   // this layer's output bound terms (rounded up: bounds of the f32 sums)
+            float lk = 0.0f, bk = 0.0f;
+            for (int n = 0; n < NF; n++) {
+                double s = 0.0;
+                for (int i = 0; i < 9 * NF; i++) s += std::fabs((double)hwio[l][(size_t)i * NF + n]);
+                lk = std::max(lk, (float)(s * (1.0 + 1e-6)));
+                bk = std::max(bk, std::fabs(biases[l][n]));
+            }
+            hdr[4] = lk;
+            hdr[5] = bk;
+            hdr[6] = hdr[7] = 0.0f;
+        }
         for (int tap = 0; tap < 9; tap++)
             for (int c = 0; c < NF; c++)
                 for (int n = 0; n < NF; n++) {
@@ -1382,10 +1498,16 @@ static void set_tower_attrs()
     SDE_X6P_ATTR(false, false, false, true);
     SDE_X6P_ATTR(false, true, true, false);
     SDE_X6P_ATTR(false, true, false, false);
+    (void)hipFuncSetAttribute((const void *)conv64_x6p_kernel<true, false, false, false, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, XP_SMEM);
 #undef SDE_X6P_ATTR1
 #undef SDE_X6P_ATTR
-#define SDE_H16_ATTR(L, I, O, S) (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<L, I, O, S>, \
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM)
+#define SDE_H16_ATTR(L, I, O, S, ...) (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<L, I, O, S, ##__VA_ARGS__>, \
+                                                                hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM)
+    SDE_H16_ATTR(false, false, false, false, true, true);
+    (void)hipFuncSetAttribute((const void *)conv64_h16q_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM);
+    SDE_H16_ATTR(true, false, false, false, true, false);
+    SDE_H16_ATTR(true, false, false, true, true, false);
     SDE_H16_ATTR(true, true, false, false);
     SDE_H16_ATTR(true, false, false, false);
     SDE_H16_ATTR(true, true, false, true);
@@ -1430,7 +1552,7 @@ static int cu_count()
 static void launch_layer(const float *in, int Hin, int Win, const float *packed, int nlayers, int layer, float *out,
                          int flags, uint16_t *ohi, uint16_t *olo, float *onrm, bool in_cb, bool out_cb,
                          const float *in_amax, float *out_amax, hipStream_t st, int nimg = 1, int64_t in_stride = 0,
-                         int64_t out_stride = 0, int amax_stride = 0)
+                         int64_t out_stride = 0, int amax_stride = 0, bool in_sp = false, bool out_sp = false)
 {
     set_tower_attrs();
     const bool last = (layer == nlayers);
@@ -1474,10 +1596,17 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         bt.pix_stride = (int64_t)hout * wout;
         bt.amax_stride = amax_stride;
         const int grid = std::min(bt.ntiles, cu_count());
-#define SDE_H16(L, I, O, S) conv64_h16_kernel<L, I, O, S><<<grid, 512, H16_SMEM, st>>>(in, Hin, Win, wk, out, hout, wout, \
-                                                                                       (S) ? ohi : nullptr, (S) ? olo : nullptr, \
-                                                                                       (S) ? onrm : nullptr, bt, in_amax, out_amax)
+#define SDE_H16(L, I, O, S, ...) conv64_h16_kernel<L, I, O, S, ##__VA_ARGS__><<<grid, 512, H16_SMEM, st>>>( \
+        in, Hin, Win, wk, out, hout, wout, (S) ? ohi : nullptr, (S) ? olo : nullptr, (S) ? onrm : nullptr, bt, in_amax, out_amax)
         const bool split = ohi || olo || onrm;
+        if (in_sp) {   // split activations in (and out, below the last layer): LDS-DMA stagers
+            if (!last && SDE_H16Q)   // the 4-wave kernel with resident weights (tower_h16q.h)
+                conv64_h16q_kernel<<<grid, 256, H16_SMEM, st>>>(in, Hin, Win, wk, out, hout, wout, bt, in_amax, out_amax);
+            else if (!last) SDE_H16(false, false, false, false, true, true);
+            else if (split) SDE_H16(true, false, false, true, true, false);
+            else SDE_H16(true, false, false, false, true, false);
+            return;
+        }
         if (last && split) { if (in_cb) SDE_H16(true, true, false, true); else SDE_H16(true, false, false, true); }
         else if (last) { if (in_cb) SDE_H16(true, true, false, false); else SDE_H16(true, false, false, false); }
         else if (in_cb) { if (out_cb) SDE_H16(false, true, true, false); else SDE_H16(false, true, false, false); }
@@ -1495,9 +1624,13 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         bt.pix_stride = (int64_t)hout * wout;
         bt.amax_stride = amax_stride;
         const int grid = std::min(bt.ntiles, cu_count());
-#define SDE_X6P(F, L, I, O, H) conv64_x6p_kernel<F, L, I, O, H><<<grid, 512, XP_SMEM, st>>>( \
+#define SDE_X6P(F, L, I, O, H, ...) conv64_x6p_kernel<F, L, I, O, H, ##__VA_ARGS__><<<grid, 512, XP_SMEM, st>>>( \
         in, Hin, Win, (F) ? w1 : nullptr, wk, out, hout, wout, (L) ? ohi : nullptr, (L) ? olo : nullptr, \
         (L) ? onrm : nullptr, bt, in_amax, out_amax)
+        if (out_sp) {   // layer 2 writing split activations (f16x3; the callers check)
+            SDE_X6P(true, false, false, false, true, true);
+            return;
+        }
 #define SDE_X6P_ALL(H)                                                      \
         if (layer == 2) {                                                   \
             if (last) SDE_X6P(true, true, false, false, H);                 \
@@ -1532,8 +1665,35 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
     }
 }
 
+// split activations (SDE_TOWER_IN_SPLIT / OUT_SPLIT): the scale word sits at bound word + XP_SCALE_WORD (so
+// the bound-word arrays hold 64 words per image and a tower at most 32 layers), and a plane's bytes
+// (h w 16) times 8 fit the 32-bit buffer offsets
+static constexpr int64_t SPLIT_MAX_PIX = (int64_t)1 << 24;
+#ifndef SDE_SPLIT_ACT
+// 1: sde_tower_forward* pass split activations between the f16x3 64->64 layers (conv64_h16q_kernel in the
+// middle); 0 (the default): fp32 c-blocks.  Same time within 0.5 % on MI355X (the tower is
+// power-capped, and the split path moves the fp16 split from the stagers into the MFMA waves' epilogue);
+// ops.TOWER_SPLIT_ACT mirrors this for the layer-by-layer drivers.
+#define SDE_SPLIT_ACT 0
+#endif
+static bool split_ok(int nlayers, int64_t pix) { return nlayers <= XP_SCALE_WORD && pix < SPLIT_MAX_PIX; }
+// the kernels that exist: layer 2 may write split planes; a middle layer reads them iff it writes them; the
+// last layer may read them
+static bool split_pairing_ok(bool in_sp, bool out_sp, int layer, int nlayers, int64_t pix)
+{
+    if (!in_sp && !out_sp) return true;
+    if (!split_ok(nlayers, pix) || (in_sp && layer == 2) || (out_sp && layer == nlayers)) return false;
+    return layer == 2 || layer == nlayers || in_sp == out_sp;
+}
+
 static bool tower_flags_ok(int flags, bool layer_api)
 {
+    if (flags & (SDE_TOWER_IN_SPLIT | SDE_TOWER_OUT_SPLIT)) {   // F16X3 on the 16x16x32 kernel (layer API only)
+        if (!layer_api || !(flags & SDE_TOWER_F16X3) || (flags & (SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32))) return false;
+        if ((flags & SDE_TOWER_IN_SPLIT && flags & SDE_TOWER_IN_CBLOCK) ||
+            (flags & SDE_TOWER_OUT_SPLIT && flags & SDE_TOWER_OUT_CBLOCK)) return false;
+        flags &= ~(SDE_TOWER_IN_SPLIT | SDE_TOWER_OUT_SPLIT);
+    }
     if (flags & (SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32)) {   // F16X3 only: the 64 -> 64 layers' kernel choice
         if (!(flags & SDE_TOWER_F16X3) || (flags & SDE_TOWER_WINOGRAD && flags & SDE_TOWER_MFMA32)) return false;
         flags &= ~(SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32);
@@ -1557,8 +1717,10 @@ SDE_EXPORT int sde_tower_layer_scaled(const float *in, int Hin, int Win, const f
     if ((in_cb && layer == 2) || (out_cb && layer == nlayers)) return SDE_ERR_ARG;
     if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
     if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax))) return SDE_ERR_ARG;
+    const bool in_sp = (flags & SDE_TOWER_IN_SPLIT) != 0, out_sp = (flags & SDE_TOWER_OUT_SPLIT) != 0;
+    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, (int64_t)Hin * Win)) return SDE_ERR_ARG;
     launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, in_cb, out_cb,
-                 in_absmax, out_absmax, as_stream(stream));
+                 in_absmax, out_absmax, as_stream(stream), 1, 0, 0, 0, in_sp, out_sp);
     return launch_status();
 }
 
@@ -1578,8 +1740,12 @@ SDE_EXPORT int sde_tower_layer_batch(const float *in, int nimg, int64_t in_strid
                      (layer == nlayers && out_stride != hout * wout * NF))) return SDE_ERR_ARG;
     if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax) || (nimg > 1 && amax_stride < 1)))
         return SDE_ERR_ARG;
+    const bool in_sp = (flags & SDE_TOWER_IN_SPLIT) != 0, out_sp = (flags & SDE_TOWER_OUT_SPLIT) != 0;
+    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, (int64_t)Hin * Win) ||
+        ((in_sp || out_sp) && nimg > 1 && amax_stride <= XP_SCALE_WORD))
+        return SDE_ERR_ARG;
     launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, nullptr, nullptr, nullptr, in_cb, out_cb,
-                 in_absmax, out_absmax, as_stream(stream), nimg, in_stride, out_stride, amax_stride);
+                 in_absmax, out_absmax, as_stream(stream), nimg, in_stride, out_stride, amax_stride, in_sp, out_sp);
     return launch_status();
 }
 
@@ -1651,18 +1817,21 @@ SDE_EXPORT int sde_tower_forward_batch(const float *img_pad, int nimg, int H, in
         absmax_kernel<<<dim3(blocks, nimg), 256, 0, st>>>(img_pad, img_stride, amax, AS);
     }
     int hin = Hp, win = Wp;
-    // intermediate activations in the c-block-major layout on the split paths
-    const bool cbl = (flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) != 0;
+    // intermediate activations: f16x3 on the 16x16x32 kernel -- split (scaled fp16 parts, staged by LDS-DMA);
+    // the other split paths -- c-block-major fp32
+    const bool sp = SDE_SPLIT_ACT && f16 && !(flags & (SDE_TOWER_WINOGRAD | SDE_TOWER_MFMA32)) && nlayers > 2 &&
+                    split_ok(nlayers, h2 * w2);
+    const bool cbl = !sp && (flags & (SDE_TOWER_BF16X6 | SDE_TOWER_F16X3)) != 0;
     launch_layer(img_pad, hin, win, packed, nlayers, 2, nlayers == 2 ? feat : buf[0], flags, feat_hi, feat_lo, feat_norm,
                  false, cbl && nlayers > 2, amax, amax + 1, st, nimg, img_stride,
-                 nlayers == 2 ? feat_stride : act_stride, AS);
+                 nlayers == 2 ? feat_stride : act_stride, AS, false, sp);
     hin -= 4; win -= 4;
     int cur = 0;
     for (int l = 3; l <= nlayers; l++) {
         float *o = (l == nlayers) ? feat : buf[cur ^ 1];
         launch_layer(buf[cur], hin, win, packed, nlayers, l, o, flags, feat_hi, feat_lo, feat_norm, cbl,
                      cbl && l < nlayers, amax + (l - 2), amax + (l - 1), st, nimg, act_stride,
-                     l == nlayers ? feat_stride : act_stride, AS);
+                     l == nlayers ? feat_stride : act_stride, AS, sp, sp && l < nlayers);
         hin -= 2; win -= 2;
         cur ^= 1;
     }

@@ -161,6 +161,67 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
     }
 }
 
+// Stager waves, split inputs (ISPL, SDE_TOWER_IN_SPLIT): a stage's 8 planes (part, quarter) are copies of
+// input planes cb * 8 + (part * 4 + quarter) of the tile's 18 x 34 window, each [h][w][8 fp16] in HBM -- so a
+// stage is filled by LDS-DMA with no arithmetic and no VGPR round trip: 1 KB (64 pixels, row-wrapped by the
+// per-lane source offsets) per wave-instruction, stager wave w copying planes 2w and 2w + 1, 10
+// instructions each (the last one 36 lanes).  The descriptor ends at the plane's end: a window pixel past the
+// input's right edge reads the next row's pixel, one past the plane's end reads zero; both feed only
+// outputs outside the image, which are never stored.  Same step / barrier pattern as h16_stager_loop.
+__device__ __forceinline__ void h16_dma_stager_loop(char *hsm, const float *__restrict__ in, int Hin, int Win,
+                                                    const XpBatch &bt, int st)
+{
+    const int tile0 = blockIdx.x, gstride = gridDim.x;
+    const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * H16_NCB;
+    const int w = __builtin_amdgcn_readfirstlane(st >> 6), lane = st & 63;
+    constexpr int ND = (XP_NPIX + 63) / 64, NLAST = XP_NPIX - 64 * (ND - 1);
+    uint32_t voff[ND];
+#pragma unroll
+    for (int d = 0; d < ND; d++) {
+        const int px = d * 64 + lane, iy = px / XP_IX, ix = px - iy * XP_IX;
+        voff[d] = (H16_DIAG & 32) ? (uint32_t)(((iy * (Win / 32) + (ix >> 5)) * 16) * 512 + (ix & 31) * 16)
+                                  : (uint32_t)((iy * Win + ix) * 16);
+    }
+    const size_t PB = (size_t)Hin * Win * 16;
+    auto issue = [&](int k) {
+        const int t = tile0 + (k >> 1) * gstride, cb = k & 1;
+        int img, ty0, tx0;
+        xp_tile(bt, t, img, ty0, tx0);
+        const size_t org = ((size_t)ty0 * Win + tx0) * 16;
+        const char *src = reinterpret_cast<const char *>(in + img * bt.in_stride) + (size_t)cb * 8 * PB + org;
+        char *dst = hsm + (k & 1) * H16_STAGE;
+#pragma unroll
+        for (int pp = 0; pp < 2; pp++) {
+            const int p = 2 * w + pp;
+            __amdgpu_buffer_rsrc_t rs = xp_rsrc_n(src + p * PB, (uint32_t)(PB - org));
+            if (H16_DIAG & 32) {   // timing probe: blocked layout [h][w / 32][16 planes][32][16 B]
+                const size_t o2 = ((size_t)(ty0 * (Win / 32) + (tx0 >> 5)) * 16 + cb * 8 + p) * 512;
+                rs = xp_rsrc_n(reinterpret_cast<const char *>(in + img * bt.in_stride) + o2, (uint32_t)(16 * PB - o2));
+            }
+            auto *lds = (__attribute__((address_space(3))) char *)(dst + p * H16_PLANE);
+#pragma unroll
+            for (int d = 0; d < ND - 1; d++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds + d * 1024, 16, voff[d], 0, 0, 0);
+            if (lane < NLAST) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds + (ND - 1) * 1024, 16, voff[ND - 1], 0, 0, 0);
+        }
+    };
+    if (H16_DIAG & 2) {
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < nsteps; i++) __syncthreads();
+        return;
+    }
+    issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 1
+    for (int i = 0; i < nsteps; i++) {
+        if (i + 1 < nsteps) issue(i + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
 // A fragments of one half-tap (tap s >> 1, quarters 2 (s & 1) + qq) of 32-channel c-block cb: [part][qq],
 // by buffer loads: ra = the layer's F16 A-fragment blob, voff = the lane's byte offset in its
 // [mtile][cblock16][tap][part][lane][8] order, cbo = cb's byte offset (wave-uniform); the rest of the
@@ -244,13 +305,15 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[3], 
 // Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
 // (+ the running bound word), or (LAST) the L2 norm and [h][w][64] stores.  Stored registers are
 // pinned live for XP_PIN stores, as in xp_epilogue ("store-data overwrite").
-template <bool LAST, bool OUT_CB, bool SPLIT>
+template <bool LAST, bool OUT_CB, bool SPLIT, bool OSPL>
 __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane, int g, int img, int ty0, int tx0,
                                              float unscale, const float4 *lbias4, float *__restrict__ out, int Hout,
                                              int Wout, const XpBatch &bt, uint16_t *__restrict__ ohi,
                                              uint16_t *__restrict__ olo, float *__restrict__ onrm,
-                                             uint32_t &amax_run, int &amax_img, float *__restrict__ out_amax)
+                                             uint32_t &amax_run, int &amax_img, float *__restrict__ out_amax,
+                                             float oscale)
 {
+    static_assert(!OSPL || (!LAST && !OUT_CB), "split outputs: intermediate layers");
     int j = lane & 15, k4 = lane >> 4;
     asm volatile("" : "+v"(j), "+v"(k4));
     const int row0 = 4 * g;
@@ -260,13 +323,21 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
         uint32_t amax = 0u;
         float *const outi = out + img * bt.out_stride;
         const size_t HW = (size_t)Hout * Wout;
+        // OSPL: channels 16q + 4 k4 + e are 8-channel group 2q + (k4 >> 1), plane (q >> 1) * 8 + part * 4 +
+        // 2 (q & 1) + (k4 >> 1).  A lane pair (k4 even, k4 + 1) swaps halves (v_permlane16_swap, rows 2i <->
+        // 2i + 1) so that the even lane holds the group's 8 hi parts and the odd one its 8 lo parts: one 16-B
+        // store each, to plane part = k4 & 1
+        const uint32_t pb = (uint32_t)HW * 16u;
+        const uint32_t ospl_lane = (uint32_t)((k4 & 1) * 4 + (k4 >> 1)) * pb;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float4 b4 = lbias4[4 * q + k4];
             const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
             // OUT_CB: [cblk16 = q][h][w][16], one descriptor per c-block plane; else [h][w][64]
-            const __amdgpu_buffer_rsrc_t rs = xp_rsrc(OUT_CB ? outi + ((size_t)q * HW + (size_t)ty0 * Wout) * 16
-                                                             : outi + (size_t)ty0 * Wout * NF);
+            const __amdgpu_buffer_rsrc_t rs =
+                OSPL ? xp_rsrc(reinterpret_cast<char *>(outi) + ((size_t)((q >> 1) * 8 + 2 * (q & 1)) * HW + (size_t)ty0 * Wout) * 16)
+                     : xp_rsrc(OUT_CB ? outi + ((size_t)q * HW + (size_t)ty0 * Wout) * 16
+                                      : outi + (size_t)ty0 * Wout * NF);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const bool rok = ty0 + row0 + r < Hout;   // wave-uniform
@@ -281,14 +352,44 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                     for (int e = 0; e < 4; e++) o4[e] = fmaxf(fmaf(c[e], unscale, bq[e]), 0.f);
                     const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                     const int k = (q * 4 + r) * 2 + ph;
-                    pin[k] = __builtin_bit_cast(u32x4, o);
-                    if (rok) {
-                        if (xok) {   // the bound before the store: nothing writes o's registers after it
-                            amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
-                            amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                    if (OSPL) {
+                        f16x4 hv, lv;
+                        xp_split16(o, oscale, hv, lv);
+                        u32x2 hw2 = __builtin_bit_cast(u32x2, hv), lw2 = __builtin_bit_cast(u32x2, lv);
+#pragma unroll
+                        for (int w = 0; w < 2; w++) {   // odd rows' hi <-> even rows' lo
+                            const auto sw = __builtin_amdgcn_permlane16_swap(hw2[w], lw2[w], false, false);
+                            hw2[w] = sw[0];
+                            lw2[w] = sw[1];
                         }
-                        if (!(H16_DIAG & 1)) xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
-                               so);
+                        const u32x4 v4 = {hw2.x, hw2.y, lw2.x, lw2.y};
+                        pin[k] = v4;
+                        if (rok) {
+                            if (xok) {
+                                amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                                amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                            }
+                            const uint32_t v2 = xok ? ospl_lane + (uint32_t)x * 16u : XP_OOB;
+                            const uint32_t s2 = (uint32_t)((row0 + r) * Wout) * 16u;
+                            if (H16_DIAG & 16) {   // timing probe: blocked layout (last partial block column skipped)
+                                if (tx0 + 32 <= Wout) {
+                                    const int P = (q >> 1) * 8 + 2 * (q & 1) + (k4 & 1) * 4 + (k4 >> 1);
+                                    const uint32_t a = (uint32_t)((((ty0 + row0 + r) * (Wout / 32) + (tx0 >> 5)) * 16 + P) * 512 +
+                                                                  (16 * ph + j) * 16);
+                                    __builtin_amdgcn_raw_buffer_store_b128(v4, xp_rsrc(outi), a, 0, 0);
+                                }
+                            } else if (!(H16_DIAG & 1)) __builtin_amdgcn_raw_buffer_store_b128(v4, rs, v2, s2, 0);
+                        }
+                    } else {
+                        pin[k] = __builtin_bit_cast(u32x4, o);
+                        if (rok) {
+                            if (xok) {   // the bound before the store: nothing writes o's registers after it
+                                amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
+                                amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
+                            }
+                            if (!(H16_DIAG & 1)) xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
+                                   so);
+                        }
                     }
                     if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
                 }
@@ -380,7 +481,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
 // Layers 3..L, f16x3; IN_CB / OUT_CB: c-block-major activations [cblk16][h][w][16] (the tower's
 // intermediate layout) or [h][w][64]; LAST writes the [h][w][64] features (+ the optional split
 // planes and norm bounds: SPLIT, the last layer only).
-template <bool LAST, bool IN_CB, bool OUT_CB, bool SPLIT>
+template <bool LAST, bool IN_CB, bool OUT_CB, bool SPLIT, bool ISPL = false, bool OSPL = false>
 __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ wkblob, float *__restrict__ out,
                                                          int Hout, int Wout, uint16_t *__restrict__ ohi,
@@ -395,9 +496,11 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     if (tile >= bt.ntiles) return;
     const float *hdr = wkblob + LK_F16 + LK_W;
     if (wave >= 4) {
-        h16_stager_loop<IN_CB>(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr);
+        if (ISPL) h16_dma_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS);
+        else h16_stager_loop<IN_CB>(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr);
         return;
     }
+    if (OSPL) xp_publish_scale(false, bt, in_amax, hdr, out_amax);
     const int g = __builtin_amdgcn_readfirstlane(wave);
     float *lbias = reinterpret_cast<float *>(hsm + H16_BIAS_OFF);
     if (wave == 0) lbias[lane] = wkblob[lane];   // published by the first barrier below
@@ -418,7 +521,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     }
 
     int sc_img = -1;
-    float sc_u = 1.0f;
+    float sc_u = 1.0f, sc_o = 1.0f;
     uint32_t amax_run = 0u;
     int amax_img = -1;
     int cur = 0;
@@ -433,12 +536,18 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
             h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             if (cb == H16_NCB - 1) {
                 if (img != sc_img) {
-                    float s_unused;
-                    xp_scales(false, in_amax + img * bt.amax_stride, hdr, s_unused, sc_u);
+                    const float *am = in_amax + img * bt.amax_stride;
+                    if (ISPL) {   // the writer's published 2^sigma
+                        sc_u = hdr[0] / am[XP_SCALE_WORD];
+                    } else {
+                        float s_unused;
+                        xp_scales(false, am, hdr, s_unused, sc_u);
+                    }
+                    if (OSPL) sc_o = xp_out_scale(false, am, hdr);
                     sc_img = img;
                 }
-                h16_epilogue<LAST, OUT_CB, SPLIT>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi, olo,
-                                           onrm, amax_run, amax_img, out_amax);
+                h16_epilogue<LAST, OUT_CB, SPLIT, OSPL>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi,
+                                                       olo, onrm, amax_run, amax_img, out_amax, sc_o);
             }
             __syncthreads();
             cur ^= 1;

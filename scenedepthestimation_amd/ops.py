@@ -322,19 +322,52 @@ def absmax_batch(x, out):
     return out
 
 
-def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
-                in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
-    """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
-    in_cblock / out_cblock (bf16x6, f16x3): intermediate activations in the c-block-major layout
-    [nf/16][h][w][16] that tower_forward uses between layers (tensors keep their [h, w, nf]
-    shape; only the element order differs).
-    in_absmax / out_absmax (f16x3): f32 [1] device words -- a bound of |input| (|image| for layer
-    2) and the word this layer maxes its outputs into (zeroed by the caller)."""
-    flags = TOWER_PRECISIONS[precision]
+SCALE_WORD = 32   # split activations: 2^sigma at bound word + 32 (sde.h SDE_TOWER_OUT_SPLIT)
+# whether sde_tower_forward* pass split activations between the default f16x3 tower's 64->64 layers
+# (tower.hip SDE_SPLIT_ACT; the layer-by-layer drivers in pipeline.py follow it to stay bit-identical)
+TOWER_SPLIT_ACT = False
+
+
+def _layout_flags(flags, in_cblock, out_cblock, in_split, out_split):
     if in_cblock:
         flags |= _lib.SDE_TOWER_IN_CBLOCK
     if out_cblock:
         flags |= _lib.SDE_TOWER_OUT_CBLOCK
+    if in_split:
+        flags |= _lib.SDE_TOWER_IN_SPLIT
+    if out_split:
+        flags |= _lib.SDE_TOWER_OUT_SPLIT
+    return flags
+
+
+def _check_scale_word(words, rows, name):
+    """Split activations read / write words[i * stride + 32]: the storage behind the word view must hold it."""
+    if words is None:
+        return
+    stride = words.stride(0) if words.dim() > 1 else 0
+    last = words.storage_offset() + (rows - 1) * stride + SCALE_WORD
+    if words.untyped_storage().nbytes() < (last + 1) * 4:
+        raise ValueError(f"{name}: split activations need the bound-word array to extend {SCALE_WORD} words "
+                         "past each image's word (the scale word)")
+
+
+def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "fp32", split=None,
+                in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None,
+                in_split: bool = False, out_split: bool = False):
+    """One tower layer = one kernel launch (layer 2 = conv1+conv2 fused from the padded image).
+    in_cblock / out_cblock (bf16x6, f16x3): intermediate activations in the c-block-major layout
+    [nf/16][h][w][16] that tower_forward uses between layers (tensors keep their [h, w, nf]
+    shape; only the element order differs).
+    in_split / out_split (f16x3): the split-activation layout the default f16x3 tower_forward uses between
+    layers (16 planes [cblk32][part][quarter] of [h][w][8 fp16], same bytes as [h, w, nf] f32); the scale
+    2^sigma travels at in_absmax / out_absmax + 32 (views into a >= 33-word array).
+    in_absmax / out_absmax (f16x3): f32 [1] device words -- a bound of |input| (|image| for layer
+    2) and the word this layer maxes its outputs into (zeroed by the caller)."""
+    flags = _layout_flags(TOWER_PRECISIONS[precision], in_cblock, out_cblock, in_split, out_split)
+    if in_split:
+        _check_scale_word(in_absmax, 1, "in_absmax")
+    if out_split:
+        _check_scale_word(out_absmax, 1, "out_absmax")
     if layer == 2:
         Hin, Win = inp.shape
         oshape = (Hin - 4, Win - 4, nf)
@@ -352,15 +385,17 @@ def tower_layer(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precis
 
 
 def tower_layer_batch(inp, packed, nlayers: int, layer: int, out, nf: int = 64, precision: str = "f16x3",
-                      in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None):
+                      in_cblock: bool = False, out_cblock: bool = False, in_absmax=None, out_absmax=None,
+                      in_split: bool = False, out_split: bool = False):
     """tower_layer over a batch per launch: inp [N, Hin, Win] (layer 2) or [N, Hin, Win, nf], out
-    [N, h, w, nf]; in_absmax / out_absmax (f16x3): [N, k] device words, column 0 used (row stride k)."""
-    flags = TOWER_PRECISIONS[precision]
-    if in_cblock:
-        flags |= _lib.SDE_TOWER_IN_CBLOCK
-    if out_cblock:
-        flags |= _lib.SDE_TOWER_OUT_CBLOCK
+    [N, h, w, nf]; in_absmax / out_absmax (f16x3): [N, k] device words, column 0 used (row stride k;
+    k > 32 with split activations, whose scale word is column 32)."""
+    flags = _layout_flags(TOWER_PRECISIONS[precision], in_cblock, out_cblock, in_split, out_split)
     N, Hin, Win = inp.shape[:3]
+    if in_split:
+        _check_scale_word(in_absmax, N, "in_absmax")
+    if out_split:
+        _check_scale_word(out_absmax, N, "out_absmax")
     sh = 4 if layer == 2 else 2
     oshape = (N, Hin - sh, Win - sh, nf)
     ws = 0

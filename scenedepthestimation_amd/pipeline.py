@@ -23,6 +23,7 @@ from . import mc_cnn, ops
 
 
 AMAX_WORDS = 64   # f16x3 bound words per image in the tower workspace (TOWER_AMAX_BYTES / 4)
+SPLIT_MAX_PIX = 1 << 24   # split activations: fewer input pixels per plane than this (tower.hip SPLIT_MAX_PIX)
 # Placement draws of the four SGM volumes (StereoMatcher._place_sgm_volumes): volumes of [MIN, MAX] voxels are
 # placed by up to this many allocate-and-time draws (larger ones would hold three 4-volume sets of > 6 GB each).
 SGM_PLACEMENT_TRIALS = 8
@@ -47,8 +48,11 @@ def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3"
     need = ops.tower_batch_workspace_bytes(H, W, N, L, nf)
     if ws.numel() < need:
         raise ValueError("tower workspace too small")
-    cbl = precision in ("bf16x6", "f16x3", "f16x3w", "f16x3m32")
     h2, w2 = H + 2 * (L - 2), W + 2 * (L - 2)
+    # between layers: what sde_tower_forward_batch passes -- split activations on the f16x3 tower when
+    # built with them (ops.TOWER_SPLIT_ACT; <= 32 layers, < 2^24 pixels), else c-block-major fp32
+    sp = ops.TOWER_SPLIT_ACT and precision == "f16x3" and 2 < L <= ops.SCALE_WORD and h2 * w2 < SPLIT_MAX_PIX
+    cbl = not sp and precision in ("bf16x6", "f16x3", "f16x3w", "f16x3m32")
     act = h2 * w2 * nf if L > 2 else 0
     wsf = ws[: 2 * N * act * 4 + N * AMAX_WORDS * 4].view(torch.float32)
     bufs = [wsf[: N * act], wsf[N * act: 2 * N * act]]
@@ -69,7 +73,7 @@ def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3"
     first = out if L == 2 else bufs[0][: N * hin * win * nf].view(N, hin, win, nf)
     run(2, lambda: ops.tower_layer_batch(img_pad, packed, L, 2, first, nf=nf, precision=precision,
                                          out_cblock=cbl and L > 2, in_absmax=words[:, 0:1] if f16 else None,
-                                         out_absmax=words[:, 1:2] if (f16 and L > 2) else None))
+                                         out_absmax=words[:, 1:2] if (f16 and L > 2) else None, out_split=sp))
     cur = 0
     for layer in range(3, L + 1):
         yield layer - 1, words
@@ -78,7 +82,8 @@ def tower_steps(img_pad, packed, nlayers: int, out, ws, precision: str = "f16x3"
         run(layer, lambda: ops.tower_layer_batch(src, packed, L, layer, o, nf=nf, precision=precision,
                                                  in_cblock=cbl, out_cblock=cbl and layer < L,
                                                  in_absmax=words[:, layer - 2:layer - 1] if f16 else None,
-                                                 out_absmax=words[:, layer - 1:layer] if (f16 and layer < L) else None))
+                                                 out_absmax=words[:, layer - 1:layer] if (f16 and layer < L) else None,
+                                                 in_split=sp, out_split=sp and layer < L))
         hin, win = hin - 2, win - 2
         cur ^= 1
 

@@ -52,7 +52,7 @@ def test_tower_packing_matches_layout():
     packed = ops.pack_tower_weights(hw, hb)
     LW = 9 * 64 * 64
     LF = 64 + LW + 3 * LW // 2                    # bias | f32 [tap][n][c] | 3 bf16 parts
-    LWINO = LF + LW + 4                           # | 2 fp16 parts of W * 2^tau | F16 header
+    LWINO = LF + LW + 8                           # | 2 fp16 parts of W * 2^tau | F16 header (8 floats)
     LK = LWINO + 16 * 64 * 64 + 4                 # | 2 fp16 parts of U * 2^tau_u (Winograd) | header
     assert packed.size == ops.tower_packed_floats(L) == 64 + 576 + 2 * LK
     assert np.array_equal(packed[:64], hb[0])
@@ -73,9 +73,11 @@ def test_tower_packing_matches_layout():
         assert np.array_equal(as_f32.sum(0), ref.astype(np.float64))
         hi = as_f32[0]
         assert np.all(np.abs(ref - hi) <= np.abs(ref) * 2.0 ** -8)
-        # F16X3: header {2^-tau, conv1 L1 bound, max |b1|, 0}; two fp16 parts of W * 2^tau in the
-        # same fragment order with 2 parts, max |W| * 2^tau in [2^14, 2^15)
-        hdr = packed[base + LF + LW:base + LK]
+        # F16X3: header {2^-tau, conv1 L1 bound, max |b1|, 0, L1 bound, max |b|, 0, 0}; two fp16 parts of
+        # W * 2^tau in the same fragment order with 2 parts, max |W| * 2^tau in [2^14, 2^15)
+        hdr = packed[base + LF + LW:base + LWINO]
+        lk = np.abs(hw[l].reshape(9 * 64, 64).astype(np.float64)).sum(0).max()   # max_n sum_{tap,c} |w|
+        assert lk <= hdr[4] <= lk * (1 + 4e-6) and hdr[5] == np.abs(hb[l]).max() and hdr[6] == hdr[7] == 0
         tau = -int(np.log2(hdr[0]))
         assert hdr[0] == 2.0 ** -tau and 2.0 ** 14 <= np.abs(ref).max() * 2.0 ** tau < 2.0 ** 15
         l1 = np.abs(hw[0].reshape(9, 64).astype(np.float64)).sum(0).max()
@@ -129,6 +131,15 @@ def test_argument_validation_without_gpu():
     assert lib.sde_tower_layer_scaled(1, 8, 8, 1, 5, 64, 3, 1, 9, N, N, N, 1, 1, N) == ERR         # two precisions
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 9, N, N, N, N) == ERR           # two precisions
     assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 8 | 2, N, N, N, N) == ERR       # layout flag
+    assert lib.sde_tower_forward(1, 8, 8, 1, 5, 64, 1, 1, 1 << 30, 8 | 128, N, N, N, N) == ERR     # split flag
+    scaled = lambda layer, flags, L=5: lib.sde_tower_layer_scaled(1, 8, 8, 1, L, 64, layer, 1, flags, N, N, N, 1, 1, N)
+    assert scaled(3, 64) == ERR                         # split activations without f16x3
+    assert scaled(2, 8 | 64) == ERR                     # layer 2 reads the image
+    assert scaled(5, 8 | 128) == ERR                    # the last layer writes features
+    assert scaled(3, 8 | 64) == ERR and scaled(3, 8 | 128) == ERR   # a middle layer: both or neither
+    assert scaled(3, 8 | 64 | 128 | 2) == ERR           # IN_SPLIT with IN_CBLOCK
+    assert scaled(3, 8 | 64 | 128 | 32) == ERR          # with the 32x32x16 kernel
+    assert scaled(3, 8 | 64 | 128, L=33) == ERR         # the scale word needs <= 32 layers
     assert lib.sde_absmax_f32(N, 4, 1, N) == ERR
     assert lib.sde_feature_split(1, 10, 32, 1, 1, 1, N) == ERR                                     # C != 64
     assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace

@@ -257,22 +257,71 @@ def test_tower_layer_api_matches_forward(gpu):
     packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=9), L)))
     img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
     img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
-    for prec, cbl in (("fp32", False), ("bf16x6", False), ("bf16x6", True), ("f16x3", False), ("f16x3", True),
-                      ("f16x3w", False), ("f16x3w", True), ("f16x3m32", False), ("f16x3m32", True)):
+    for prec, lay in (("fp32", "hw"), ("bf16x6", "hw"), ("bf16x6", "cb"), ("f16x3", "hw"), ("f16x3", "cb"),
+                      ("f16x3", "split"), ("f16x3w", "hw"), ("f16x3w", "cb"), ("f16x3m32", "hw"), ("f16x3m32", "cb")):
         full = ops.tower_forward(img, packed, L, precision=prec)
         x = img
-        words = torch.zeros(L, device="cuda")          # f16x3 bound words, as tower_forward keeps them
+        words = torch.zeros(64, device="cuda")         # f16x3 bound words (+ the split scale words at +32)
         ops.absmax(img, words[0:1])
+        cbl, sp = lay == "cb", lay == "split"
         for layer in range(2, L + 1):
             shrink = 4 if layer == 2 else 2
             y = torch.empty((x.shape[0] - shrink, x.shape[1] - shrink, 64), device="cuda")
             ops.tower_layer(x, packed, L, layer, y, precision=prec, in_cblock=cbl and layer > 2,
                             out_cblock=cbl and layer < L, in_absmax=words[layer - 2:layer - 1],
-                            out_absmax=words[layer - 1:layer] if layer < L else None)
+                            out_absmax=words[layer - 1:layer] if layer < L else None,
+                            in_split=sp and layer > 2, out_split=sp and layer < L)
             x = y
         torch.cuda.synchronize()
-        # same arithmetic in the same order whatever the activation layout: bit-identical
-        assert torch.equal(x, full), (prec, cbl)
+        if prec == "f16x3" and sp != ops.TOWER_SPLIT_ACT:
+            # split activations take their scalings from a-priori bounds instead of the measured maxima:
+            # a different rounding of the same fp32-level arithmetic than tower_forward's layout
+            err = float((x - full).abs().max())
+            assert err < 2e-6, (prec, lay, err)
+        else:
+            # same arithmetic in the same order whatever the activation layout: bit-identical
+            assert torch.equal(x, full), (prec, lay)
+
+
+def test_tower_split_activation_layout(gpu):
+    """SDE_TOWER_OUT_SPLIT: layer 2's outputs as 16 planes [cblk32][part][quarter] of [h][w][8 fp16] --
+    (hi + lo) / 2^sigma reproduces the fp32 layer output within the split's 2^-22 relative + 2^-25 / 2^sigma
+    absolute bound, the bound word is the fp32 path's exactly, 2^sigma is published at word + 32 and keeps
+    |hi| < 2^15 (no overflow); the next (last) layer reading the split planes (IN_SPLIT) matches the
+    fp32-input layer to fp32-level error."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    L, H, W = 3, 70, 90
+    rng = np.random.default_rng(21)
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=2), L)))
+    img = torch.zeros((H + 2 * L, W + 2 * L), device="cuda")
+    img[L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32)).cuda()
+    h2, w2 = H + 2 * L - 4, W + 2 * L - 4
+    wa, wb = torch.zeros(64, device="cuda"), torch.zeros(64, device="cuda")
+    ops.absmax(img, wa[0:1])
+    ops.absmax(img, wb[0:1])
+    ya = torch.empty((h2, w2, 64), device="cuda")
+    yb = torch.empty((h2, w2, 64), device="cuda")
+    ops.tower_layer(img, packed, L, 2, ya, precision="f16x3", in_absmax=wa[0:1], out_absmax=wa[1:2])
+    ops.tower_layer(img, packed, L, 2, yb, precision="f16x3", in_absmax=wb[0:1], out_absmax=wb[1:2], out_split=True)
+    torch.cuda.synchronize()
+    assert wa[1].item() == wb[1].item() > 0                       # the measured bound word
+    s = wb[1 + 32].item()
+    sigma = int(np.log2(s))
+    assert s == 2.0 ** sigma and wa[33].item() == 0
+    planes = host(yb).view(np.float16).reshape(2, 2, 4, h2, w2, 8).astype(np.float64)   # [cb][part][q][h][w][8]
+    hi, lo = planes[:, 0], planes[:, 1]
+    assert np.abs(hi).max() < 2.0 ** 15
+    val = (hi + lo).transpose(2, 3, 0, 1, 4).reshape(h2, w2, 64)                         # -> [h][w][cb q e]
+    ref = host(ya).astype(np.float64) * s
+    assert np.all(np.abs(val - ref) <= np.abs(ref) * 2.0 ** -22 + 2.0 ** -25)
+    # the next layer from either layout
+    za = torch.empty((h2 - 2, w2 - 2, 64), device="cuda")
+    zb = torch.empty((h2 - 2, w2 - 2, 64), device="cuda")
+    ops.tower_layer(ya, packed, L, 3, za, precision="f16x3", in_absmax=wa[1:2])
+    ops.tower_layer(yb, packed, L, 3, zb, precision="f16x3", in_absmax=wb[1:2], in_split=True)
+    torch.cuda.synchronize()
+    err = float((za - zb).abs().max())       # L2-normalised features
+    assert err <= 2e-6, err
 
 
 def test_tower_winograd_large_plane_takes_direct_kernel(gpu):
@@ -854,8 +903,10 @@ def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
         single = ops.tower_forward(imgs[i].contiguous(), packed, L, precision=precision)
         assert torch.equal(out[i], single), (precision, i)
     if L >= 2:
-        cbl = precision != "fp32"
-        words = torch.zeros((N, 8), device="cuda")
+        # the forward's inter-layer layout: split activations on the default f16x3 tower, c-blocks otherwise
+        sp = ops.TOWER_SPLIT_ACT and precision == "f16x3" and L > 2
+        cbl = precision != "fp32" and not sp
+        words = torch.zeros((N, 64), device="cuda")
         for i in range(N):
             ops.absmax(imgs[i], words[i, 0:1])
         x = imgs
@@ -864,9 +915,40 @@ def test_tower_forward_batch_equals_single(gpu, precision, nlayers, H, W, N):
             y = torch.empty((N, x.shape[1] - sh, x.shape[2] - sh, 64), device="cuda")
             ops.tower_layer_batch(x, packed, L, layer, y, precision=precision, in_cblock=cbl and layer > 2,
                                   out_cblock=cbl and layer < L, in_absmax=words[:, layer - 2:layer - 1],
-                                  out_absmax=words[:, layer - 1:layer] if layer < L else None)
+                                  out_absmax=words[:, layer - 1:layer] if layer < L else None,
+                                  in_split=sp and layer > 2, out_split=sp and layer < L)
             x = y
         assert torch.equal(x, out)
+
+
+def test_tower_split_chain_batch_many_tiles(gpu):
+    """Split activations chained over a batch with more tiles than CUs (the 4-wave middle-layer kernel's
+    persistent tile loop, its one-step-ahead LDS-DMA across tiles and images, partial edge tiles): the
+    features match the c-block forward to fp32 level for images of very different dynamic range."""
+    from scenedepthestimation_amd import mc_cnn, ops
+    L, H, W, N = 5, 400, 700, 2
+    rng = np.random.default_rng(8)
+    packed = dev(ops.pack_tower_weights(*mc_cnn.layer_lists(mc_cnn.synthetic_weights(L, seed=6), L)))
+    imgs = torch.zeros((N, H + 2 * L, W + 2 * L), device="cuda")
+    for i in range(N):
+        imgs[i, L:-L, L:-L] = torch.from_numpy(rng.standard_normal((H, W)).astype(np.float32) * 10.0 ** (3 * i)).cuda()
+    ref = ops.tower_forward_batch(imgs, packed, L, precision="f16x3")
+    words = torch.zeros((N, 64), device="cuda")
+    for i in range(N):
+        ops.absmax(imgs[i], words[i, 0:1])
+    x = imgs
+    for layer in range(2, L + 1):
+        sh = 4 if layer == 2 else 2
+        y = torch.empty((N, x.shape[1] - sh, x.shape[2] - sh, 64), device="cuda")
+        ops.tower_layer_batch(x, packed, L, layer, y, precision="f16x3", in_absmax=words[:, layer - 2:layer - 1],
+                              out_absmax=words[:, layer - 1:layer] if layer < L else None,
+                              in_split=layer > 2, out_split=layer < L)
+        x = y
+    torch.cuda.synchronize()
+    assert torch.isfinite(x).all()
+    err = float((x - ref).abs().max())
+    print("split chain vs c-block forward", err)
+    assert err < 2e-6, err
 
 
 def test_preprocess_and_absmax_batch(gpu):

@@ -20,6 +20,10 @@ hin, win = H + 6, W + 6
 x = torch.rand((hin, win, 64), device="cuda")
 y = torch.empty((hin - 2, win - 2, 64), device="cuda")
 words = torch.ones(2, device="cuda")
+# split-activation input of layer 3 (fp16 parts in [0, 1), as 16 planes) and a 64-word bound array whose
+# scale word (32) holds 2^0
+xs = torch.rand((hin * win * 128,), device="cuda").half().view(torch.float32).view(hin, win, 64)
+words64 = torch.ones(64, device="cuda")
 imgs = torch.randn((2, H + 2 * L, W + 2 * L), device="cuda")
 feat = torch.empty((2, H, W, 64), device="cuda")
 nws = ops.tower_batch_workspace_bytes(H, W, 2, L)
@@ -51,11 +55,13 @@ res = {}
 for rnd in range(3):
     for name, lib in libs:
         s = torch.cuda.current_stream().cuda_stream
-        for prec, flag in (("f16x3", 8), ("f16x3 m32", 8 | 32)):
+        for prec, flag in (("f16x3", 8 | 2 | 4), ("f16x3 m32", 8 | 32 | 2 | 4), ("f16x3 split", 8 | 64 | 128)):
             def run():
-                rc = lib.sde_tower_layer_scaled(x.data_ptr(), hin, win, packed.data_ptr(), L, 64, 3, y.data_ptr(),
-                                                flag | 2 | 4, None, None, None, words.data_ptr(),
-                                                words.data_ptr() + 4, s)
+                sp = flag & 64
+                rc = lib.sde_tower_layer_scaled((xs if sp else x).data_ptr(), hin, win, packed.data_ptr(), L, 64, 3,
+                                                y.data_ptr(), flag, None, None, None,
+                                                (words64 if sp else words).data_ptr(),
+                                                (words64 if sp else words).data_ptr() + 4, s)
                 assert rc == 0, rc
             res.setdefault((name, "layer3 " + prec), []).append(timed(run, 20))
             if "clk" in name and rnd == 0:   # TOWER_DIAG & 128: per-workgroup cycle / 100 MHz-tick deltas
