@@ -773,16 +773,35 @@ __device__ __forceinline__ void xp_cblock(floatx16 (&acc)[XP_ACC], XpFrag (&a)[8
     }
 }
 
-// o * s (s = 2^sigma) split exactly into two fp16 parts: hi = fp16(o s), lo = fp16(o s - hi)
-__device__ __forceinline__ void xp_split16(float4 o, float s, f16x4 &hv, f16x4 &lv)
+// x (already scaled by 2^sigma) split exactly into two fp16 parts: hi = fp16(x) (v_cvt_pk_f16_f32), lo =
+// fp16(x - hi) by v_fma_mix{lo,hi}_f16 straight from the packed hi half (x - hi is exact in fp32, so its one
+// rounding gives the bits of (fp16)(x - (float)hi); 6 instructions per 4 values instead of 12)
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void xp_split16s(float4 x, u32x2 &hw, u32x2 &lw)
 {
-    const float xs[4] = {o.x * s, o.y * s, o.z * s, o.w * s};
+    const f16x2 h01 = {(_Float16)x.x, (_Float16)x.y}, h23 = {(_Float16)x.z, (_Float16)x.w};
+    hw = u32x2{__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23)};
+    uint32_t l01, l23;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(l01) : "v"(x.x), "v"(hw.x));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l01) : "v"(x.y), "v"(hw.x));
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(l23) : "v"(x.z), "v"(hw.y));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l23) : "v"(x.w), "v"(hw.y));
+    lw = u32x2{l01, l23};
+}
+
+// a lane pair (rows 2i, 2i + 1 of 16 lanes: SWAP32 = false; halves of 32: true) trades halves so that the
+// even lane ends with both lanes' hi parts and the odd one with both lo parts (odd lanes' hi <-> even lanes' lo)
+template <bool SWAP32>
+__device__ __forceinline__ u32x4 xp_pair_parts(u32x2 hw, u32x2 lw)
+{
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const _Float16 hh = (_Float16)xs[e];
-        hv[e] = hh;
-        lv[e] = (_Float16)(xs[e] - (float)hh);
+    for (int w = 0; w < 2; w++) {
+        const auto sw = SWAP32 ? __builtin_amdgcn_permlane32_swap(hw[w], lw[w], false, false)
+                               : __builtin_amdgcn_permlane16_swap(hw[w], lw[w], false, false);
+        hw[w] = sw[0];
+        lw[w] = sw[1];
     }
+    return u32x4{hw.x, hw.y, lw.x, lw.y};
 }
 
 // Tile epilogue of one MFMA wave (output rows WR*g .., M-tiles mt0 ..): bias (+ReLU | L2-normalise),
@@ -861,25 +880,21 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
                         const int q = 2 * qh + ql;
                         const float bq[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
                         float o4[4];
+                        // OSPL: the outputs scaled by 2^sigma straight from the accumulators (the scale folded
+                        // into the unscale and the bias: exact, powers of two), their bound unscaled at the flush
+                        const float us = OSPL ? unscale * oscale : unscale;
 #pragma unroll
                         for (int e = 0; e < 4; e++)
-                            o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], unscale, bq[e]) : c[4 * q + e] + bq[e]), 0.f);
+                            o4[e] = fmaxf((F16 ? fmaf(c[4 * q + e], us, OSPL ? bq[e] * oscale : bq[e]) : c[4 * q + e] + bq[e]), 0.f);
                         const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                         const int k = ((m * 2 + qh) * XP_WROWS + r) * 2 + ql;
                         if (OSPL) {
-                            // scaled fp16 parts of channels 32 (mt0 + m) + 8q + 4h ..: the lane pair (h = 0, 1)
-                            // swaps halves (v_permlane32_swap) so that lane h = 0 holds the group's 8 hi parts
-                            // and h = 1 its 8 lo parts: one 16-B store each, to plane (mt0 + m) * 8 + h * 4 + q
-                            f16x4 hv, lv;
-                            xp_split16(o, oscale, hv, lv);
-                            u32x2 hw2 = __builtin_bit_cast(u32x2, hv), lw2 = __builtin_bit_cast(u32x2, lv);
-#pragma unroll
-                            for (int w = 0; w < 2; w++) {   // upper half's hi <-> lower half's lo
-                                const auto sw = __builtin_amdgcn_permlane32_swap(hw2[w], lw2[w], false, false);
-                                hw2[w] = sw[0];
-                                lw2[w] = sw[1];
-                            }
-                            const u32x4 v4 = {hw2.x, hw2.y, lw2.x, lw2.y};
+                            // fp16 parts of channels 32 (mt0 + m) + 8q + 4h ..: the lane pair (h = 0, 1) swaps
+                            // halves (v_permlane32_swap) so that lane h = 0 holds the group's 8 hi parts and
+                            // h = 1 its 8 lo parts: one 16-B store each, to plane (mt0 + m) * 8 + h * 4 + q
+                            u32x2 hw2, lw2;
+                            xp_split16s(o, hw2, lw2);
+                            const u32x4 v4 = xp_pair_parts<true>(hw2, lw2);
                             pin[k] = v4;
                             if (rok) {
                                 amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
@@ -908,6 +923,8 @@ __device__ __forceinline__ void xp_epilogue(const floatx16 (&acc)[XP_ACC], int l
 #pragma unroll
         for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
         asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+        if (OSPL)   // the bound of the scaled outputs, unscaled (exact: a power of two)
+            amax = __float_as_uint(__uint_as_float(amax) / oscale);
         if (F16) {
             if (!xok) amax = 0u;   // lanes past the output edge stored nothing
             // one atomic per wave and image (flushed when the tiles move to the next

@@ -348,21 +348,17 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                     const bool xok = x < Wout;
                     const floatx4 &c = acc[(r * 2 + ph) * 4 + q];
                     float o4[4];
+                    // OSPL: the outputs scaled by 2^sigma straight from the accumulators (scale folded into
+                    // the unscale and the bias: exact), their bound unscaled below
 #pragma unroll
-                    for (int e = 0; e < 4; e++) o4[e] = fmaxf(fmaf(c[e], unscale, bq[e]), 0.f);
+                    for (int e = 0; e < 4; e++)
+                        o4[e] = fmaxf(fmaf(c[e], OSPL ? unscale * oscale : unscale, OSPL ? bq[e] * oscale : bq[e]), 0.f);
                     const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                     const int k = (q * 4 + r) * 2 + ph;
                     if (OSPL) {
-                        f16x4 hv, lv;
-                        xp_split16(o, oscale, hv, lv);
-                        u32x2 hw2 = __builtin_bit_cast(u32x2, hv), lw2 = __builtin_bit_cast(u32x2, lv);
-#pragma unroll
-                        for (int w = 0; w < 2; w++) {   // odd rows' hi <-> even rows' lo
-                            const auto sw = __builtin_amdgcn_permlane16_swap(hw2[w], lw2[w], false, false);
-                            hw2[w] = sw[0];
-                            lw2[w] = sw[1];
-                        }
-                        const u32x4 v4 = {hw2.x, hw2.y, lw2.x, lw2.y};
+                        u32x2 hw2, lw2;
+                        xp_split16s(o, hw2, lw2);
+                        const u32x4 v4 = xp_pair_parts<false>(hw2, lw2);
                         pin[k] = v4;
                         if (rok) {
                             if (xok) {
@@ -398,6 +394,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
 #pragma unroll
         for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
         asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+        if (OSPL) amax = __float_as_uint(__uint_as_float(amax) / oscale);   // exact: a power of two
         // one atomic per wave and image (flushed when the tiles move to the next image and at the end)
         if (img != amax_img) {
             xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);

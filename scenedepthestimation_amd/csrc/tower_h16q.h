@@ -142,8 +142,9 @@ constexpr int H16Q_STORES = 32;   // epilogue stores per lane per tile (all issu
 __device__ __forceinline__ void h16q_epilogue(const floatx4 (&acc)[32], int lane, int g, int img, int ty0, int tx0,
                                               float unscale, const float4 (&b4)[H16Q_NQ], float oscale,
                                               float *__restrict__ out, int Hout, int Wout, const XpBatch &bt,
-                                              uint32_t &amax)
+                                              uint32_t &amax_run)
 {
+    uint32_t amax = 0u;
     int j = lane & 15, k4 = lane >> 4;
     asm volatile("" : "+v"(j), "+v"(k4));
     const size_t HW = (size_t)Hout * Wout;
@@ -158,7 +159,10 @@ __device__ __forceinline__ void h16q_epilogue(const floatx4 (&acc)[32], int lane
         const int q = q0 + qq;
         const __amdgpu_buffer_rsrc_t rs =
             xp_rsrc(outi + ((size_t)((q >> 1) * 8 + 2 * (q & 1)) * HW + (size_t)(ty0 + r0) * Wout) * 16);
-        const float bq[4] = {b4[qq].x, b4[qq].y, b4[qq].z, b4[qq].w};
+        // the outputs scaled by 2^sigma straight from the accumulators (scale folded into the unscale and
+        // the bias: exact), their bound unscaled at the end
+        const float bq[4] = {b4[qq].x * oscale, b4[qq].y * oscale, b4[qq].z * oscale, b4[qq].w * oscale};
+        const float us = unscale * oscale;
 #pragma unroll
         for (int r = 0; r < H16Q_NR; r++) {
             const bool rok = ty0 + r0 + r < Hout;
@@ -170,23 +174,16 @@ __device__ __forceinline__ void h16q_epilogue(const floatx4 (&acc)[32], int lane
                 const floatx4 &c = acc[(r * 2 + ph) * H16Q_NQ + qq];
                 float o4[4];
 #pragma unroll
-                for (int e = 0; e < 4; e++) o4[e] = fmaxf(fmaf(c[e], unscale, bq[e]), 0.f);
+                for (int e = 0; e < 4; e++) o4[e] = fmaxf(fmaf(c[e], us, bq[e]), 0.f);
                 const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
                 if (ok) {   // the bound before the store: nothing writes o's registers after it
                     amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
                     amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
                 }
-                f16x4 hv, lv;
-                xp_split16(o, oscale, hv, lv);
-                u32x2 hw2 = __builtin_bit_cast(u32x2, hv), lw2 = __builtin_bit_cast(u32x2, lv);
-#pragma unroll
-                for (int w = 0; w < 2; w++) {   // odd rows' hi <-> even rows' lo
-                    const auto sw = __builtin_amdgcn_permlane16_swap(hw2[w], lw2[w], false, false);
-                    hw2[w] = sw[0];
-                    lw2[w] = sw[1];
-                }
+                u32x2 hw2, lw2;
+                xp_split16s(o, hw2, lw2);
                 const int k = (qq * H16Q_NR + r) * 2 + ph;
-                pin[k] = u32x4{hw2.x, hw2.y, lw2.x, lw2.y};
+                pin[k] = xp_pair_parts<false>(hw2, lw2);
                 __builtin_amdgcn_raw_buffer_store_b128(pin[k], rs, ok ? lane_pl + (uint32_t)x * 16u : XP_OOB, so, 0);
                 if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
             }
@@ -195,6 +192,8 @@ __device__ __forceinline__ void h16q_epilogue(const floatx4 (&acc)[32], int lane
 #pragma unroll
     for (int k = 32 - (XP_PIN - 1); k + 1 < 32; k++) asm volatile("" ::"v"(pin[k]));
     asm volatile("s_nop 4" ::"v"(pin[31]));
+    // the bound of the scaled outputs, unscaled (exact: a power of two)
+    amax_run = max(amax_run, __float_as_uint(__uint_as_float(amax) / oscale));
 }
 
 // Middle layers, split in and out.  wkblob: the layer's packed blob; in_amax / out_amax: the bound words
