@@ -15,7 +15,8 @@
  *     compute_feature returns, process_functional.py:42-43);
  *   - return value: SDE_OK or a negative sde_status; errors are detected before
  *     any launch (argument checks) or right after it (hipGetLastError).
- *   - reentrant: no global state besides the HIP module the loader registers.
+ *   - reentrant: no global state besides the HIP module the loader registers and the
+ *     tower's grid cap (sde_set_persistent_grid, a tuning knob that does not change results).
  */
 #ifndef SDE_H
 #define SDE_H
@@ -133,6 +134,12 @@ int sde_argmin_merge(const float *mins, const int32_t *args, int nshards, int64_
 /* MC-CNN-fast branch (mc_cnn_brunch.py:31-48; compute_feature's sess.run,   */
 /* process_functional.py:11-45).  nlayers 3x3 VALID convs, nf = 64 maps.     */
 /* ---------------------------------------------------------------------- */
+
+/* Workgroups of the persistent tower kernels (default 0: one per CU of the device).  A positive value caps
+ * the grid -- for a tower sharing the device with other work on CU-masked streams (hipExtStreamCreateWithCUMask),
+ * where one workgroup per device CU would leave the last ones waiting for the other stream's CUs.  Process-wide;
+ * results do not depend on it. */
+int sde_set_persistent_grid(int cus);
 
 /* Tower arithmetic (flags of sde_tower_forward / sde_tower_layer). */
 #define SDE_TOWER_FP32 0      /* v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation            */

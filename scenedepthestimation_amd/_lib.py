@@ -65,6 +65,7 @@ SIGNATURES = {
     "sde_tower_layer_batch": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_int, c_int, c_int,
                                       c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "sde_absmax_f32": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "sde_set_persistent_grid": (c_int, [c_int]),
     "sde_absmax_f32_batch": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p]),
     "sde_preprocess_u8_batch": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sde_preprocess_u8": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -20,6 +20,8 @@
 //   parts, six partial products on v_mfma_f32_32x32x16_bf16 -- see below.
 #include "sde_common.h"
 
+#include <atomic>
+
 #include <vector>
 
 #include <algorithm>
@@ -1546,6 +1548,11 @@ static void set_tower_attrs()
     });
 }
 
+// Persistent tower grids: one workgroup per CU (160 KB of LDS each), or g_grid_cus workgroups when set
+// (sde_set_persistent_grid: the tower sharing the device with other work on CU-masked streams, where a
+// workgroup per device CU would leave the last ones waiting for CUs the other stream holds).
+static std::atomic<int> g_grid_cus{0};
+
 static int cu_count()
 {
     static int cached[64] = {0};
@@ -1556,7 +1563,8 @@ static int cu_count()
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
         cached[dev] = n;
     }
-    return cached[dev];
+    const int g = g_grid_cus.load(std::memory_order_relaxed);
+    return g > 0 ? std::min(g, cached[dev]) : cached[dev];
 }
 
 // One launch: layer == 2 -> conv1+conv2 fused from the padded image (Hin x Win floats);
@@ -1773,6 +1781,13 @@ SDE_EXPORT int sde_tower_layer(const float *in, int Hin, int Win, const float *p
     if (flags & SDE_TOWER_F16X3) return SDE_ERR_ARG;   // needs the bound words: sde_tower_layer_scaled
     return sde_tower_layer_scaled(in, Hin, Win, packed, nlayers, nf, layer, out, flags, feat_hi, feat_lo, feat_norm,
                                   nullptr, nullptr, stream);
+}
+
+SDE_EXPORT int sde_set_persistent_grid(int cus)
+{
+    if (cus < 0) return SDE_ERR_ARG;
+    g_grid_cus.store(cus, std::memory_order_relaxed);
+    return SDE_OK;
 }
 
 SDE_EXPORT int sde_absmax_f32(const float *x, int64_t n, float *absmax, void *stream)

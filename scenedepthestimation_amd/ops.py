@@ -283,6 +283,12 @@ def absmax(x, out):
     return out
 
 
+def set_persistent_grid(cus: int = 0):
+    """Cap the persistent tower kernels' grid at `cus` workgroups (0: one per device CU), for a tower that
+    shares the device with work on CU-masked streams (sde_set_persistent_grid)."""
+    check(lib.sde_set_persistent_grid(int(cus)), "sde_set_persistent_grid")
+
+
 def tower_batch_workspace_bytes(H: int, W: int, nimg: int, nlayers: int, nf: int = 64) -> int:
     return int(lib.sde_tower_batch_workspace_bytes(H, W, nimg, nlayers, nf))
 
