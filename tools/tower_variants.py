@@ -55,7 +55,8 @@ res = {}
 for rnd in range(3):
     for name, lib in libs:
         s = torch.cuda.current_stream().cuda_stream
-        for prec, flag in (("f16x3", 8 | 2 | 4), ("f16x3 m32", 8 | 32 | 2 | 4), ("f16x3 split", 8 | 64 | 128)):
+        for prec, flag in (("f16x3", 8 | 2 | 4), ("f16x3 m32", 8 | 32 | 2 | 4), ("f16x3 split", 8 | 64 | 128),
+                           ("f16x3 wino", 8 | 16 | 2 | 4)):
             def run():
                 sp = flag & 64
                 rc = lib.sde_tower_layer_scaled((xs if sp else x).data_ptr(), hin, win, packed.data_ptr(), L, 64, 3,
@@ -69,10 +70,11 @@ for rnd in range(3):
                 print(f"{name:20s} {prec}: in-kernel clock {(st[:, 0] / st[:, 1] * 0.1).median().item():.3f} GHz, "
                       f"{st[:, 0].median().item() / 1e3:.0f} kcycles", flush=True)
 
-        def runb():
+        def runb(flags=8):
             rc = lib.sde_tower_forward_batch(imgs.data_ptr(), 2, H, W, packed.data_ptr(), L, 64, feat.data_ptr(),
-                                             ws.data_ptr(), nws, 8, None, None, None, s)
+                                             ws.data_ptr(), nws, flags, None, None, None, s)
             assert rc == 0, rc
+        res.setdefault((name, "tower pair f16x3w"), []).append(timed(lambda: runb(8 | 16), 10))
         res.setdefault((name, "tower pair f16x3"), []).append(timed(runb, 10))
         if rnd == 0:   # features bit-identical to the first library's
             runb()
