@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(256) void conv1_only_kernel(const float *__restrict
 // image (np.getbufsize()); mean = S / n in float32; std = sqrt(S' / n) with S' the same reduction
 // of (x - mean)^2 (float32 ops, no contraction: the library is built with -ffp-contract=off).
 // Pinned against NumPy in tests (test_preprocess_u8: bit-identical at every config size).
-// Scratch per image: [mean, std, -, -][one float per piece].
+// Scratch per image: [mean, std, -, -][piece sums][piece sums of squares].
 constexpr int NP_PIECE = 8192;
 
 __device__ __forceinline__ float np_val(const uint8_t *img, int64_t i, float mean, bool sq)
@@ -1237,13 +1237,47 @@ __device__ __forceinline__ int np_half(int len) { const int n2 = len / 2; return
 // perfect tree of 64 blocks of 128 (lane l sums block l; the xor-butterfly adds adjacent subtrees,
 // and float addition is commutative); the last, short piece walks numpy's recursion: every lane
 // enumerates the blocks in order (lane k % 64 sums block k into LDS), lane 0 adds them up the tree.
+// S = 0.0f + v[0] + v[1] + ... in order (np.mean's / np.std's float32 reduction of the piece sums), then the
+// quotient: the wave loads the sums into LDS (one round of latency), lane 0 adds them.  NumPy 2.x divides
+// the float32 sum by the intp count in float64 and rounds once to float32 (np.mean: ret.dtype.type(ret /
+// rcount); _var: true_divide by an intp into a float32 out, and its final ret / rcount), so the quotient
+// is formed in fp64 here too.  Below 2^24 pixels this equals the float32 quotient S / (float)n (fp64 has
+// more than 2 * 24 + 2 bits: the double rounding is innocuous); above it (float)n would be inexact.
+__device__ __forceinline__ float np_stat(const float *__restrict__ v, int npieces, int64_t n, float *buf, int lane)
+{
+    float q = 0.0f;
+    for (int c0 = 0; c0 < npieces; c0 += 256) {   // LDS chunks of 256 sums
+        const int m = min(256, npieces - c0);
+        for (int c = lane; c < m; c += 64) buf[c] = v[c0 + c];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0)
+            for (int c = 0; c < m; c++) q += buf[c];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    q = __shfl(q, 0, 64);
+    return (float)((double)q / (double)n);
+}
+
+// SQ: the pass over (x - mean)^2, the mean formed here from the first pass's piece sums (the launch of a
+// separate statistics kernel saved); block 0 also stores it.  Scratch per image: [mean, std, -, -][piece
+// sums][piece sums of squares].
 template <bool SQ>
 __global__ __launch_bounds__(64) void np_piece_kernel(const uint8_t *__restrict__ imgs, int64_t n, int sstride,
                                                       float *__restrict__ scratch)
 {
     const uint8_t *img = imgs + blockIdx.y * n;
     float *st = scratch + (size_t)blockIdx.y * sstride;
-    const float mean = SQ ? st[0] : 0.0f;
+    const int npieces = gridDim.x;
+    __shared__ float sbuf[256];
+    float mean = 0.0f;
+    if (SQ) {
+        mean = np_stat(st + 4, npieces, n, sbuf, threadIdx.x);
+        if (blockIdx.x == 0 && threadIdx.x == 0) st[0] = mean;
+    }
     const int lane = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * NP_PIECE;
     const int m = (int)std::min<int64_t>(NP_PIECE, n - c0);
@@ -1301,44 +1335,45 @@ __global__ __launch_bounds__(64) void np_piece_kernel(const uint8_t *__restrict_
             sum = ret;
         }
     }
-    if (lane == 0) st[4 + blockIdx.x] = sum;
-}
-
-// S = 0.0f + piece 0 + piece 1 + ... in order; STAGE 0: mean = S / n, 1: std = sqrt(S / n).
-// NumPy 2.x divides the float32 sum by the intp count in float64 and rounds once to float32 (np.mean:
-// ret.dtype.type(ret / rcount); _var: true_divide by an intp into a float32 out, and its final
-// ret / rcount), so the quotient is formed in fp64 here too.  Below 2^24 pixels this equals the
-// float32 quotient S / (float)n (fp64 has more than 2 * 24 + 2 bits: the double rounding is
-// innocuous); above it (float)n would be inexact.
-template <int STAGE>
-__global__ __launch_bounds__(64) void np_stat_kernel(float *__restrict__ scratch, int sstride, int npieces, int64_t n)
-{
-    if (threadIdx.x != 0) return;
-    float *st = scratch + (size_t)blockIdx.x * sstride;
-    float S = 0.0f;
-    for (int c = 0; c < npieces; c++) S += st[4 + c];
-    const float q = (float)((double)S / (double)n);
-    st[STAGE] = STAGE == 0 ? q : sqrtf(q);
+    if (lane == 0) st[4 + (SQ ? npieces : 0) + blockIdx.x] = sum;
 }
 
 // (I - mean) / std in float32 (match_single.py:40-41), zero border (process_functional.py:13-19).
+constexpr int ZN_PER = 8;   // padded pixels per thread of znorm_pad_kernel
+
+// The std formed here (every block, from the second pass's piece sums: np_stat by its first wave) -- the
+// launch of a separate statistics kernel saved; block 0 stores it in the scratch's std word.
 __global__ __launch_bounds__(256) void znorm_pad_kernel(const uint8_t *__restrict__ img, int H, int W, int pad,
-                                                        const float *__restrict__ scratch, int sstride,
+                                                        float *__restrict__ scratch, int sstride, int npieces,
                                                         float *__restrict__ out)
 {
     const int Wp = W + 2 * pad;
     img += (size_t)blockIdx.y * H * W;      // batch: image blockIdx.y
-    const float *st = scratch + (size_t)blockIdx.y * sstride;
+    float *st = scratch + (size_t)blockIdx.y * sstride;
     out += (size_t)blockIdx.y * (H + 2 * pad) * Wp;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)(H + 2 * pad) * Wp) return;
-    const float mean = st[0], stdv = st[1];
-    // the padded image has < 2^31 pixels (checked by sde_preprocess_u8_batch)
-    const int ii = (int)i;
-    const int y = ii / Wp - pad, x = ii % Wp - pad;
-    float v = 0.0f;
-    if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - mean) / stdv;
-    out[i] = v;
+    __shared__ float sbuf[256];
+    __shared__ float sstd;
+    if (threadIdx.x < 64) {
+        const float v = sqrtf(np_stat(st + 4 + npieces, npieces, (int64_t)H * W, sbuf, threadIdx.x));
+        if (threadIdx.x == 0) {
+            sstd = v;
+            if (blockIdx.x == 0) st[1] = v;
+        }
+    }
+    __syncthreads();
+    const float mean = st[0], stdv = sstd;
+    const int64_t np_ = (int64_t)(H + 2 * pad) * Wp;
+#pragma unroll
+    for (int k = 0; k < ZN_PER; k++) {   // ZN_PER pixels per thread: the block's statistics amortised
+        const int64_t i = ((int64_t)blockIdx.x * ZN_PER + k) * blockDim.x + threadIdx.x;
+        if (i >= np_) break;
+        // the padded image has < 2^31 pixels (checked by sde_preprocess_u8_batch)
+        const int ii = (int)i;
+        const int y = ii / Wp - pad, x = ii % Wp - pad;
+        float v = 0.0f;
+        if (y >= 0 && y < H && x >= 0 && x < W) v = ((float)img[(size_t)y * W + x] - mean) / stdv;
+        out[i] = v;
+    }
 }
 
 }  // namespace sde
@@ -1882,7 +1917,7 @@ SDE_EXPORT int64_t sde_preprocess_scratch_bytes(int H, int W)
 {
     if (H <= 0 || W <= 0) return -1;
     const int64_t pieces = ((int64_t)H * W + NP_PIECE - 1) / NP_PIECE;
-    return ((4 + pieces) * 4 + 255) / 256 * 256;
+    return ((4 + 2 * pieces) * 4 + 255) / 256 * 256;
 }
 
 SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int W, int pad, float *out_pad,
@@ -1897,10 +1932,9 @@ SDE_EXPORT int sde_preprocess_u8_batch(const uint8_t *imgs, int nimg, int H, int
     const int sstride = (int)(sde_preprocess_scratch_bytes(H, W) / 4);
     float *sc = reinterpret_cast<float *>(scratch);
     np_piece_kernel<false><<<dim3(pieces, nimg), 64, 0, st>>>(imgs, npix, sstride, sc);
-    np_stat_kernel<0><<<nimg, 64, 0, st>>>(sc, sstride, pieces, npix);
     np_piece_kernel<true><<<dim3(pieces, nimg), 64, 0, st>>>(imgs, npix, sstride, sc);
-    np_stat_kernel<1><<<nimg, 64, 0, st>>>(sc, sstride, pieces, npix);
-    znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256), nimg), 256, 0, st>>>(imgs, H, W, pad, sc, sstride, out_pad);
+    znorm_pad_kernel<<<dim3((unsigned)cdiv(n, 256 * ZN_PER), nimg), 256, 0, st>>>(imgs, H, W, pad, sc, sstride, pieces,
+                                                                                  out_pad);
     return launch_status();
 }
 

@@ -146,8 +146,8 @@ def test_argument_validation_without_gpu():
     assert lib.sde_cv_wta_split(1, 1, N, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 1 << 20, N) == ERR
     assert lib.sde_preprocess_u8(1, 4, 4, 5, 1, None, None) == ERR
     assert lib.sde_preprocess_scratch_bytes(0, 4) == -1
-    # [mean, std, -, -] + one float per 8192-pixel piece, rounded to 256 B
-    assert lib.sde_preprocess_scratch_bytes(1024, 1024) == 768 and lib.sde_preprocess_scratch_bytes(3, 5) == 256
+    # [mean, std, -, -] + two floats per 8192-pixel piece (sums, sums of squares), rounded to 256 B
+    assert lib.sde_preprocess_scratch_bytes(1024, 1024) == 1280 and lib.sde_preprocess_scratch_bytes(3, 5) == 256
     assert lib.sde_tower_packed_floats(0, 64) == -1
     W8 = lib.sde_cbca_workspace_bytes(4, 8)
     assert W8 == 4 * 8 * 4 and lib.sde_cbca_workspace_bytes(5, 7) == 4 * 7 * 8 and lib.sde_cbca_workspace_bytes(0, 7) == 0
