@@ -66,13 +66,17 @@ __device__ __forceinline__ void h16_put(char *dst, float4 v, float s)
 }
 
 // Stage unit (pixel << 2 | 4-channel chunk) of stager thread st at iteration i: a wave's lanes take 16
-// consecutive pixels x the 4 chunks (chunk = lane >> 4), so each 32-lane half of a ds_write_b64 fills one
-// quarter plane's 256 contiguous bytes (the planes are 256-B aligned: lane-contiguous units would put
-// both quarters of a pixel in one bank set), and the wave's loads still cover 1 KB of pixels contiguously.
+// consecutive pixels x the 4 chunks, so each 32-lane half of a ds_write_b64 fills one quarter plane's 256
+// contiguous bytes (the planes are 256-B aligned: lane-contiguous units would put both quarters of a pixel
+// in one bank set), and the wave's loads still cover 1 KB of pixels contiguously.  Within a half the chunk
+// pair of a pixel is the fastest index (lane = 32 plane + 16 pixel-octet + 2 pixel + chunk & 1): each
+// 16-lane group of the write is then 128 contiguous bytes, one dword per bank (pixels at a 16-B stride put
+// pixels 8 apart on one bank: 5.2e6 conflict cycles per launch by PMC, round 5).
 __device__ __forceinline__ int h16_unit(int st, int i)
 {
-    const int px = (i * (XP_STAGERS / 64) + (st >> 6)) * 16 + (st & 15);
-    return px * 4 + ((st >> 4) & 3);
+    const int l = st & 63;
+    const int px = (i * (XP_STAGERS / 64) + (st >> 6)) * 16 + ((l >> 4) & 1) * 8 + ((l >> 1) & 7);
+    return px * 4 + ((l >> 5) << 1 | (l & 1));
 }
 static_assert(XP_UPT * XP_STAGERS / 4 >= XP_NPIX, "the stager units cover the stage's pixels");
 
