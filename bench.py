@@ -595,7 +595,7 @@ def main():
                     k = 3 * 16 / 36
                 ach = k * fl / (conv_ms * 1e-3) / 1e12
                 kname = ("wino_kernel<false,true,true>" if m.tower_precision == "f16x3w" else
-                         "conv64_h16_kernel<false,true,true,false,false,false>" if m.tower_precision == "f16x3" else
+                         "conv64_h16_kernel<false,true,true,false,false,false,false>" if m.tower_precision == "f16x3" else
                          f"conv64_x6p_kernel<false,false,true,true,{str(kt == 'f16').lower()}>")
                 roof = {"kernel": f"{kname} (tower layer 3, {m.tower_precision})", "bound": "mfma",
                         "achieved": ach, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_BF16_TFLOPS,

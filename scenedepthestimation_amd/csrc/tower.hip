@@ -1135,6 +1135,9 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 #include "tower_wino.h"
 #include "tower_h16.h"
 #include "tower_h16q.h"
+#ifndef SDE_H16_L2
+#define SDE_H16_L2 1   // 0: layer 2 on conv64_x6p_kernel (32x32x16), for A/B builds
+#endif
 #ifndef SDE_H16Q
 #define SDE_H16Q 1   // 0: timing builds only -- middle split layers on conv64_h16_kernel's 8-wave form
 #endif
@@ -1560,6 +1563,12 @@ static void set_tower_attrs()
                                                                 hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM)
     SDE_H16_ATTR(false, false, false, false, true, true);
     (void)hipFuncSetAttribute((const void *)conv64_h16q_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM);
+    (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<false, false, true, false, false, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM_FIRST);
+    (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<false, false, false, false, false, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM_FIRST);
+    (void)hipFuncSetAttribute((const void *)conv64_h16_kernel<false, false, false, false, false, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, H16_SMEM_FIRST);
     SDE_H16_ATTR(true, false, false, false, true, false);
     SDE_H16_ATTR(true, false, false, true, true, false);
     SDE_H16_ATTR(true, true, false, false);
@@ -1645,6 +1654,28 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
 #undef SDE_WINO
         return;
     }
+    if (f16 && layer == 2 && !last && !(flags & SDE_TOWER_MFMA32) && SDE_H16_L2) {
+        // layer 2 (conv1 on the stagers + conv2) on v_mfma_f32_16x16x32_f16 (tower_h16.h)
+        XpBatch bt;
+        bt.tiles_x = cdiv(wout, XP_TX);
+        bt.tiles_img = bt.tiles_x * cdiv(hout, XP_TY);
+        bt.ntiles = bt.tiles_img * nimg;
+        bt.in_stride = in_stride;
+        bt.out_stride = out_stride;
+        bt.pix_stride = (int64_t)hout * wout;
+        bt.amax_stride = amax_stride;
+        const int grid = std::min(bt.ntiles, cu_count());
+        if (out_sp)
+            conv64_h16_kernel<false, false, false, false, false, true, true><<<grid, 512, H16_SMEM_FIRST, st>>>(
+                in, Hin, Win, wk, out, hout, wout, nullptr, nullptr, nullptr, bt, in_amax, out_amax, w1);
+        else if (out_cb)
+            conv64_h16_kernel<false, false, true, false, false, false, true><<<grid, 512, H16_SMEM_FIRST, st>>>(
+                in, Hin, Win, wk, out, hout, wout, nullptr, nullptr, nullptr, bt, in_amax, out_amax, w1);
+        else
+            conv64_h16_kernel<false, false, false, false, false, false, true><<<grid, 512, H16_SMEM_FIRST, st>>>(
+                in, Hin, Win, wk, out, hout, wout, nullptr, nullptr, nullptr, bt, in_amax, out_amax, w1);
+        return;
+    }
     if (f16 && layer >= 3 && !(flags & SDE_TOWER_MFMA32)) {
         // the 64 -> 64 layers on v_mfma_f32_16x16x32_f16 (tower_h16.h; same tiles as the direct kernel)
         XpBatch bt;
@@ -1657,7 +1688,8 @@ static void launch_layer(const float *in, int Hin, int Win, const float *packed,
         bt.amax_stride = amax_stride;
         const int grid = std::min(bt.ntiles, cu_count());
 #define SDE_H16(L, I, O, S, ...) conv64_h16_kernel<L, I, O, S, ##__VA_ARGS__><<<grid, 512, H16_SMEM, st>>>( \
-        in, Hin, Win, wk, out, hout, wout, (S) ? ohi : nullptr, (S) ? olo : nullptr, (S) ? onrm : nullptr, bt, in_amax, out_amax)
+        in, Hin, Win, wk, out, hout, wout, (S) ? ohi : nullptr, (S) ? olo : nullptr, (S) ? onrm : nullptr, bt, in_amax, out_amax, \
+        nullptr)
         const bool split = ohi || olo || onrm;
         if (in_sp) {   // split activations in (and out, below the last layer): LDS-DMA stagers
             if (!last && SDE_H16Q)   // the 4-wave kernel with resident weights (tower_h16q.h)

@@ -40,6 +40,10 @@ constexpr int H16_HT = 18;                                // half-taps per c-blo
 constexpr int H16_RD = 3;                                 // B ring depth (fragments read RD-1 steps ahead)
 static_assert(H16_PLANE >= XP_NPIX * 16 && H16_PLANE % 256 == 0, "plane size / bank alignment");
 static_assert(H16_SMEM <= 163840, "LDS");
+// layer 2 (FIRST): + the image window of the tile (20 x 36 fp32) behind the biases
+constexpr size_t H16_WIN_OFF = H16_SMEM;
+constexpr size_t H16_SMEM_FIRST = H16_WIN_OFF + XP_WIN * sizeof(float);   // 162,880 B
+static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
 // Timing-only diagnostic builds (tools/build_file_variant.sh tower.hip NAME -DH16_DIAG=n; wrong results):
 // 1 = no epilogue stores, 2 = stagers skip their loads and splits, 4 = MFMA waves reuse one A fragment
 // set (no A loads in the loop), 8 = wave 0 of each workgroup writes its (s_memtime, s_memrealtime) deltas
@@ -155,6 +159,116 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
     __syncthreads();
     // step i: the MFMA waves consume stage i & 1; here step i+1's halves are stored and step
     // i+2's loaded
+#pragma unroll 1
+    for (int i = 0; i < nsteps; i++) {
+        if (2 * i + 2 < nh) store(ra, 2 * i + 2);
+        if (2 * i + 4 < nh) load(ra, 2 * i + 4);
+        if (2 * i + 3 < nh) store(rb, 2 * i + 3);
+        if (2 * i + 5 < nh) load(rb, 2 * i + 5);
+        __syncthreads();
+    }
+}
+
+// Stager waves, layer 2 (FIRST): the stage is conv1 (Cin = 1, 3x3, bias, ReLU; mc_cnn_brunch.py:31-48) of
+// the padded image, computed here -- the same fmaf order as xp_conv1, so the same conv1 values as
+// conv64_x6p_kernel's layer 2.  Same units, half-steps and barriers as h16_stager_loop; a lane's 4-channel
+// chunk is the same in every unit, so a half-step's weights (9 taps + bias of 4 channels) are one register
+// set, loaded a step ahead like the activations of the other layers.  The tile's image window (20 x 36)
+// lives in LDS behind the biases, single-buffered: EVERY stager wave writes the whole window (identical
+// values) at the tile's first half-step and then reads only what it wrote itself (a wave's LDS accesses
+// complete in order), so no wave waits for another; the previous tile's window was last read in the step
+// before, which the c-block barrier closes.  The window is loaded into registers a step ahead.
+__device__ __forceinline__ void h16_conv1_stager_loop(char *hsm, const float *__restrict__ img, int Hin, int Win,
+                                                      const XpBatch &bt, int st, const float *__restrict__ in_amax,
+                                                      const float *__restrict__ hdr, const float *__restrict__ w1blob)
+{
+    const int tile0 = blockIdx.x, gstride = gridDim.x;
+    const int nsteps = ((bt.ntiles - 1 - tile0) / gstride + 1) * H16_NCB;
+    const int nh = 2 * nsteps;
+    const int lane = st & 63;
+    float *win = reinterpret_cast<float *>(hsm + H16_WIN_OFF);
+    // a unit's window offset (its top-left tap), (iy, ix) in the tile and LDS offset: tile-invariant
+    uint32_t uwin[XP_UPT], uyx[XP_UPT], ulds[XP_UPT];
+#pragma unroll
+    for (int i = 0; i < XP_UPT; i++) {
+        const int u = h16_unit(st, i), px = u >> 2, chunk = u & 3;
+        const int iy = px / XP_IX, ix = px - iy * XP_IX;
+        const bool ok = u < XP_UNITS;
+        uwin[i] = ok ? (uint32_t)(iy * XP_WX + ix) : 0u;
+        uyx[i] = ok ? (uint32_t)(iy << 16 | ix) : 0xFFFF0000u;
+        ulds[i] = ok ? (uint32_t)((chunk >> 1) * H16_PLANE + px * 16 + (chunk & 1) * 8) : 0u;
+    }
+    const int chunk = ((lane >> 5) << 1) | (lane & 1);   // = h16_unit(st, i) & 3 for every i
+    constexpr int WPL = (XP_WIN + 63) / 64;
+    float wv[WPL];
+    auto wload = [&](int t) {
+        int im, ty0, tx0;
+        xp_tile(bt, t, im, ty0, tx0);
+        const float *src = img + im * bt.in_stride;
+#pragma unroll
+        for (int k = 0; k < WPL; k++) {
+            const int idx = lane + 64 * k;
+            const int iy = idx / XP_WX, ix = idx - iy * XP_WX;
+            const int y = ty0 + iy, x = tx0 + ix;
+            wv[k] = (idx < XP_WIN && y < Hin && x < Win) ? src[(size_t)y * Win + x] : 0.0f;
+        }
+    };
+    static_assert(XP_UPT >= 10, "a half-step's weights: 9 taps + the biases");
+    // half-step k: channels 16 (k & 3) + 4 chunk .. +3; its tile's window at the tile's first half-step
+    auto load = [&](float4 (&w)[XP_UPT], int k) {
+        const int n0 = (k & 3) * 16 + chunk * 4;
+#pragma unroll
+        for (int t = 0; t < 9; t++) w[t] = *reinterpret_cast<const float4 *>(w1blob + NF + t * NF + n0);
+        w[9] = *reinterpret_cast<const float4 *>(w1blob + n0);
+        if ((k & 3) == 0) wload(tile0 + (k >> 2) * gstride);
+    };
+    int sc_img = -1;
+    float s = 1.0f, unscale = 1.0f;
+    auto store = [&](const float4 (&w)[XP_UPT], int k) {
+        int im, ty0, tx0;
+        xp_tile(bt, tile0 + (k >> 2) * gstride, im, ty0, tx0);
+        if (im != sc_img) {
+            xp_scales(true, in_amax + im * bt.amax_stride, hdr, s, unscale);
+            sc_img = im;
+        }
+        if ((k & 3) == 0) {
+#pragma unroll
+            for (int k2 = 0; k2 < WPL; k2++)
+                if (lane + 64 * k2 < XP_WIN) win[lane + 64 * k2] = wv[k2];
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the window's LDS writes have landed
+            __builtin_amdgcn_wave_barrier();
+        }
+        char *sb = hsm + ((k >> 1) & 1) * H16_STAGE + (k & 1) * 2 * H16_PLANE;
+        const int ly = Hin - 2 - ty0, lx = Win - 2 - tx0;   // conv1's output extent from the tile origin
+#pragma unroll
+        for (int i = 0; i < XP_UPT; i++) {
+            if (h16_unit(st, i) >= XP_UNITS) continue;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if ((int)(uyx[i] >> 16) < ly && (int)(uyx[i] & 0xFFFFu) < lx) {
+                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+                const float *wp = win + uwin[i];
+#pragma unroll
+                for (int t = 0; t < 9; t++) {
+                    const float x = wp[(t / 3) * XP_WX + t % 3];
+                    s0 = fmaf(x, w[t].x, s0);
+                    s1 = fmaf(x, w[t].y, s1);
+                    s2 = fmaf(x, w[t].z, s2);
+                    s3 = fmaf(x, w[t].w, s3);
+                }
+                v = make_float4(fmaxf(s0 + w[9].x, 0.f), fmaxf(s1 + w[9].y, 0.f), fmaxf(s2 + w[9].z, 0.f),
+                                fmaxf(s3 + w[9].w, 0.f));
+            }
+            h16_put(sb + ulds[i], v, s);
+        }
+    };
+    float4 ra[XP_UPT], rb[XP_UPT];
+    load(ra, 0);
+    load(rb, 1);
+    store(ra, 0);
+    store(rb, 1);
+    if (2 < nh) load(ra, 2);
+    if (3 < nh) load(rb, 3);
+    __syncthreads();
 #pragma unroll 1
     for (int i = 0; i < nsteps; i++) {
         if (2 * i + 2 < nh) store(ra, 2 * i + 2);
@@ -482,13 +596,18 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
 // Layers 3..L, f16x3; IN_CB / OUT_CB: c-block-major activations [cblk16][h][w][16] (the tower's
 // intermediate layout) or [h][w][64]; LAST writes the [h][w][64] features (+ the optional split
 // planes and norm bounds: SPLIT, the last layer only).
-template <bool LAST, bool IN_CB, bool OUT_CB, bool SPLIT, bool ISPL = false, bool OSPL = false>
+// FIRST: layer 2 -- `in` is the padded image (Hin x Win floats), w1blob conv1's weights, computed by the
+// stagers (h16_conv1_stager_loop; launch with H16_SMEM_FIRST bytes of LDS); outputs in any of the three
+// activation layouts (OSPL: the split planes).
+template <bool LAST, bool IN_CB, bool OUT_CB, bool SPLIT, bool ISPL = false, bool OSPL = false, bool FIRST = false>
 __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict__ in, int Hin, int Win,
                                                          const float *__restrict__ wkblob, float *__restrict__ out,
                                                          int Hout, int Wout, uint16_t *__restrict__ ohi,
                                                          uint16_t *__restrict__ olo, float *__restrict__ onrm, XpBatch bt,
-                                                         const float *__restrict__ in_amax, float *__restrict__ out_amax)
+                                                         const float *__restrict__ in_amax, float *__restrict__ out_amax,
+                                                         const float *__restrict__ w1blob)
 {
+    static_assert(!FIRST || (!ISPL && !SPLIT && !LAST), "layer 2: the fp32 image in, activations out");
     extern __shared__ __attribute__((aligned(16))) char hsm[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -497,11 +616,12 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     if (tile >= bt.ntiles) return;
     const float *hdr = wkblob + LK_F16 + LK_W;
     if (wave >= 4) {
-        if (ISPL) h16_dma_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS);
+        if (FIRST) h16_conv1_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr, w1blob);
+        else if (ISPL) h16_dma_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS);
         else h16_stager_loop<IN_CB>(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr);
         return;
     }
-    if (OSPL) xp_publish_scale(false, bt, in_amax, hdr, out_amax);
+    if (OSPL) xp_publish_scale(FIRST, bt, in_amax, hdr, out_amax);
     const int g = __builtin_amdgcn_readfirstlane(wave);
     float *lbias = reinterpret_cast<float *>(hsm + H16_BIAS_OFF);
     if (wave == 0) lbias[lane] = wkblob[lane];   // published by the first barrier below
@@ -542,9 +662,9 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
                         sc_u = hdr[0] / am[XP_SCALE_WORD];
                     } else {
                         float s_unused;
-                        xp_scales(false, am, hdr, s_unused, sc_u);
+                        xp_scales(FIRST, am, hdr, s_unused, sc_u);
                     }
-                    if (OSPL) sc_o = xp_out_scale(false, am, hdr);
+                    if (OSPL) sc_o = xp_out_scale(FIRST, am, hdr);
                     sc_img = img;
                 }
                 h16_epilogue<LAST, OUT_CB, SPLIT, OSPL>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi,

@@ -20,8 +20,8 @@ import subprocess
 import sys
 
 KERNELS = {   # workload -> substring of the dominant kernel's name in the counter CSV
-    "north_star": "conv64_h16_kernel<false, true, true, false, false, false>",
-    "cones": "conv64_h16_kernel<false, true, true, false, false, false>",
+    "north_star": "conv64_h16_kernel<false, true, true, false, false, false, false>",
+    "cones": "conv64_h16_kernel<false, true, true, false, false, false, false>",
     "cv": "cv_wta_row_kernel",
     "north_star_sgm": "sgm_scan_kernel",
     "c3": "sgm_scan_kernel",
