@@ -388,7 +388,8 @@ __device__ __forceinline__ floatx4 mfma16(f16x8 a, f16x8 b, floatx4 c)
 // acc[(r * 2 + ph) * 4 + q].  A ring of three half-taps with static slots (18 = 6 x 3: every c-block
 // starts in the same phase): on entry abuf[0] = A(cb, 0) and abuf[1] = A(cb, 1) are requested; half-tap s
 // requests A(s + 2) into the slot A(s - 1) left; on exit abuf[0..1] = A(ncb, 0..1).
-__device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[3], __amdgpu_buffer_rsrc_t ra,
+template <int NA>
+__device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[NA], __amdgpu_buffer_rsrc_t ra,
                                            uint32_t avoff, int cb, int ncb, const char *sb)
 {
     constexpr int NB = H16_HT * 8;
@@ -419,6 +420,61 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[3], 
         }
     }
 }
+
+// The same c-block with each B fragment feeding all four quarters (H16_B12): 9 taps x 8 (row, half) steps of
+// 12 MFMAs, so half the B reads from LDS per MFMA.  A ring of two whole taps (four half-tap slots, abuf[(h +
+// PH) % 4] for half-tap h; 18 half-taps per c-block, so the two c-blocks of a tile run in phases 0 and 2):
+// tap s requests tap s + 1 into the slots tap s - 1 left; on exit abuf holds A(ncb, tap 0) at phase PH + 2.
+// Every accumulator takes the same MFMAs in the same order as h16_cblock: the same bits.
+__device__ __forceinline__ H16B h16_bfrag12(const char *sb, int b)
+{
+    const int tap = b >> 3, r = (b >> 1) & 3, ph = b & 1;
+    const int off = ((r + tap / 3) * XP_IX + 16 * ph + tap % 3) * 16;
+    H16B f;
+    f.hi = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + off));
+    f.lo = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + 4 * H16_PLANE + off));
+    return f;
+}
+
+template <int PH>
+__device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4], __amdgpu_buffer_rsrc_t ra,
+                                             uint32_t avoff, int cb, int ncb, const char *sb)
+{
+    constexpr int NT = 9, NB = NT * 8;
+    H16B ring[2];
+    ring[0] = h16_bfrag12(sb, 0);
+#pragma unroll
+    for (int s = 0; s < NT; s++) {
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) {
+            const int h = 2 * (s + 1) + hf;
+            if (!(H16_DIAG & 4))
+                abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                                : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+        }
+#pragma unroll
+        for (int rp = 0; rp < 8; rp++) {
+            const int b = s * 8 + rp;
+            __builtin_amdgcn_sched_barrier(0);
+            const H16B &bf = ring[b & 1];
+            if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                const H16A &a = abuf[(H16_DIAG & 4) ? 0 : (2 * s + hf + PH) % 4];
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) {
+                    floatx4 &c = acc[rp * 4 + 2 * hf + qq];
+                    c = mfma16(a.f[1][qq], bf.hi, c);
+                    c = mfma16(a.f[0][qq], bf.lo, c);
+                    c = mfma16(a.f[0][qq], bf.hi, c);
+                }
+            }
+        }
+    }
+}
+#ifndef H16_B12
+#define H16_B12 1
+#endif
 
 // Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
 // (+ the running bound word), or (LAST) the L2 norm and [h][w][64] stores.  Stored registers are
@@ -631,7 +687,10 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     const uint32_t avoff = (uint32_t)((lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15)) * 16u;
     // the lane's B base: plane quarter lane >> 4, pixel (4g, lane & 15) of the input tile
     const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
-    H16A abuf[3];
+    // the middle layers' c-blocks feed each B fragment to all four quarters (h16_cblock12; layer 2 and the
+    // last layer keep h16_cblock: with their stagers / epilogue the 2-tap A ring spills 11-28 VGPRs)
+    constexpr bool B12 = H16_B12 && !LAST && !FIRST;
+    H16A abuf[4];   // h16_cblock: slots 0-2
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
     __syncthreads();
@@ -652,9 +711,14 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         floatx4 acc[32];
 #pragma unroll
         for (int i = 0; i < 32; i++) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-        for (int cb = 0; cb < H16_NCB; cb++) {
-            h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
+        // cb 0, then cb 1 and the epilogue (as a lambda: B12 unrolls the pair, the 3-slot form keeps a loop)
+        auto cstep = [&](int cb) {
+            if constexpr (B12) {
+                if (cb == 0) h16_cblock12<0>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
+                else h16_cblock12<2>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
+            } else {
+                h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
+            }
             if (cb == H16_NCB - 1) {
                 if (img != sc_img) {
                     const float *am = in_amax + img * bt.amax_stride;
@@ -672,6 +736,13 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
             }
             __syncthreads();
             cur ^= 1;
+        };
+        if constexpr (B12) {
+            cstep(0);
+            cstep(1);
+        } else {
+#pragma unroll 1
+            for (int cb = 0; cb < H16_NCB; cb++) cstep(cb);
         }
     }
     if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
