@@ -472,8 +472,10 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
         }
     }
 }
+// 2: every layer but the last one with split outputs (whose epilogue would spill), 1: the middle layers only,
+// 0: none (A/B builds)
 #ifndef H16_B12
-#define H16_B12 1
+#define H16_B12 2
 #endif
 
 // Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
@@ -687,9 +689,9 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     const uint32_t avoff = (uint32_t)((lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15)) * 16u;
     // the lane's B base: plane quarter lane >> 4, pixel (4g, lane & 15) of the input tile
     const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
-    // the middle layers' c-blocks feed each B fragment to all four quarters (h16_cblock12; layer 2 and the
-    // last layer keep h16_cblock: with their stagers / epilogue the 2-tap A ring spills 11-28 VGPRs)
-    constexpr bool B12 = H16_B12 && !LAST && !FIRST;
+    // c-blocks feeding each B fragment to all four quarters (h16_cblock12), except the last layer with
+    // split outputs (its epilogue would spill 13 VGPRs with the 2-tap A ring)
+    constexpr bool B12 = H16_B12 == 2 ? !(LAST && SPLIT) : H16_B12 == 1 ? !LAST && !FIRST : false;
     H16A abuf[4];   // h16_cblock: slots 0-2
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
