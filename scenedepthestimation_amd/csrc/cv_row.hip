@@ -324,6 +324,12 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // superstrip k-1 retired (ring = window + 4 tiles: 14 at D = 192, 112 KB).
 // ---------------------------------------------------------------------------
 constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
+#ifndef CV_FASTSPLIT
+#define CV_FASTSPLIT 15                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle (A/B builds)
+#endif
+#ifndef CV_DIAG
+#define CV_DIAG 0                          // timing-only builds (tools/cv_diag.py): phase stamps, wrong outputs
+#endif
 constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
 
 // one stager lane's 8 units (pixel u >> 4, channels 4 (u & 15) ..) of right tile T: unit u = lane + 64 i
@@ -432,6 +438,14 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     };
     load_left(0);
     __syncthreads();
+#if CV_DIAG
+    // timing-only builds: wave 0's s_memtime deltas per superstrip phase, summed, to out_disp[8 b ..]
+    uint64_t dg[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime();
+    const uint64_t tstart = tp, rstart = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&](int i) { const uint64_t t = __builtin_amdgcn_s_memtime(); dg[i] += t - tp; tp = t; };
+#else
+    auto stamp = [&](int) {};
+#endif
 
     for (int k = 0; k < nss; k++) {
         const int tlo = tlo0 + R2_NEW * k;
@@ -447,6 +461,33 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
         if (xb < W) {          // wave-uniform
             rw_f16x8 bh[4], bl[4];
             float ssl = 0.0f;
+#if CV_FASTSPLIT & 1
+            // rw_split's parts two values at a time: hi by one packed convert of the scaled pair, lo =
+            // f16(x 2^S - hi) by v_fma_mix{lo,hi} (x 2^S exact, x 2^S - hi exact in fp32: the same bits)
+            const float scl = RW_SCALE;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; s2++) {
+                const float4 a = lraw[2 * s2], b = lraw[2 * s2 + 1];
+                const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+                uint32_t hw[4], lw[4];
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    const float x0 = v8[e] * scl, x1 = v8[e + 1] * scl;
+                    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+                    const h2 hh = {(_Float16)x0, (_Float16)x1};
+                    const uint32_t hv = __builtin_bit_cast(uint32_t, hh);
+                    uint32_t lv;
+                    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lv) : "v"(x0), "v"(hv));
+                    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lv) : "v"(x1), "v"(hv));
+                    hw[e / 2] = hv;
+                    lw[e / 2] = lv;
+                    ssl += v8[e] * v8[e];
+                    ssl += v8[e + 1] * v8[e + 1];
+                }
+                bh[s2] = __builtin_bit_cast(rw_f16x8, uint4{hw[0], hw[1], hw[2], hw[3]});
+                bl[s2] = __builtin_bit_cast(rw_f16x8, uint4{lw[0], lw[1], lw[2], lw[3]});
+            }
+#else
 #pragma unroll
             for (int s2 = 0; s2 < 4; s2++) {
                 const float4 a = lraw[2 * s2], b = lraw[2 * s2 + 1];
@@ -458,13 +499,30 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     bh[s2][e] = hh;
                     bl[s2][e] = ll;
                     ssl += v8[e] * v8[e];
-                    lbad |= rw_nonfinite(v8[e]);
+                    if (!(CV_FASTSPLIT & 2)) lbad |= rw_nonfinite(v8[e]);
                 }
             }
+#endif
+#if CV_FASTSPLIT & 2
+            // a non-finite channel makes the sum of squares non-finite (an overflowing sum of finite squares
+            // is flagged too: that pixel goes to the exact fix-up, same outputs).  The other half's partial
+            // sum by the LDS shuffle (bit 8): with a permlane32 swap here the build's fix-up counts moved
+            // (693 -> 709 at 512 x 2048, same maps) -- the swap's result in lanes 0-31 was not the other
+            // half's sum in that schedule, so the norm bound would be wrong; not used
+#if CV_FASTSPLIT & 8
+            ssl += __shfl_xor(ssl, 32, 64);
+#else
+            ssl += __builtin_bit_cast(float, __builtin_amdgcn_permlane32_swap(__float_as_uint(ssl), __float_as_uint(ssl),
+                                                                              false, false)[1]);
+#endif
+            lbad = rw_nonfinite(ssl);
+#else
             ssl += __shfl_xor(ssl, 32, 64);
             lbad |= __shfl_xor((int)lbad, 32, 64) != 0;
+#endif
             nl = sqrtf(ssl) * FX_NORM_UP;
             if (more) load_left(k + 1);
+            stamp(0);
 
             float b1[4], b2[4];
             int ag[4];
@@ -581,6 +639,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     }
                 }
             }
+            stamp(1);
             // a chain that took a score holds d + t >= t >= 0; one that took none still holds -1
 #pragma unroll
             for (int t = 0; t < 4; t++) ag[t] = ag[t] >= 0 ? ag[t] - t : -1;
@@ -588,14 +647,23 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
 #pragma unroll
             for (int t = 1; t < 4; t++) fx_merge(best, arg, second, b1[t], ag[t], b2[t]);
             {
+#if CV_FASTSPLIT & 4
+                // lanes 0-31 (the ones that store) take the other half's triple by permlane32 swaps
+                auto up = [](uint32_t v) { return __builtin_amdgcn_permlane32_swap(v, v, false, false)[1]; };
+                const float bb = __uint_as_float(up(__float_as_uint(best))), ss2 = __uint_as_float(up(__float_as_uint(second)));
+                const int aa = (int)up((uint32_t)arg);
+#else
                 const float bb = __shfl_xor(best, 32, 64), ss2 = __shfl_xor(second, 32, 64);
                 const int aa = __shfl_xor(arg, 32, 64);
+#endif
                 fx_merge(best, arg, second, bb, aa, ss2);
             }
         }
+        stamp(2);
         // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
         // barrier per superstrip orders both directions
         __syncthreads();
+        stamp(3);
         if (xb < W && h == 0 && xok) {
             const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
             const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
@@ -614,7 +682,17 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 list[atomicAdd(counter, 1u)] = (int32_t)p;
             }
         }
+        stamp(4);
     }
+#if CV_DIAG
+    __syncthreads();   // every pixel's output stored: the stamps overwrite out_disp[8 b .. 8 b + 7] after them
+    if (wave == 0 && lane == 0 && out_disp) {
+        for (int i = 0; i < 5; i++) out_disp[8 * (size_t)blockIdx.x + i] = (float)dg[i];
+        out_disp[8 * (size_t)blockIdx.x + 5] = (float)(__builtin_amdgcn_s_memtime() - tstart);
+        out_disp[8 * (size_t)blockIdx.x + 6] = (float)(__builtin_amdgcn_s_memrealtime() - rstart);
+        out_disp[8 * (size_t)blockIdx.x + 7] = (float)nss;
+    }
+#endif
 }
 
 // tiles spanned by a superstrip's window and the first one (superstrip 0), floor division
