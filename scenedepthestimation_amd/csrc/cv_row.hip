@@ -325,7 +325,8 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // ---------------------------------------------------------------------------
 constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
 #ifndef CV_FASTSPLIT
-#define CV_FASTSPLIT 15                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle (A/B builds)
+#define CV_FASTSPLIT 31                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle,
+                                           // 16 the stagers' flag from the pixel norm (A/B builds)
 #endif
 #ifndef CV_DIAG
 #define CV_DIAG 0                          // timing-only builds (tools/cv_diag.py): phase stamps, wrong outputs
@@ -362,7 +363,13 @@ __device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *
         ss += rw_dpp<0x141>(ss);
         ss += rw_dpp<0x140>(ss);
         mx = max(mx, __float_as_uint(ss));          // non-negative: bit patterns order as unsigned
+#if CV_FASTSPLIT & 16
+        // a non-finite channel makes the pixel's sum of squares non-finite: one test per pixel (the norm
+        // bound then fails the certificate as well: NaN / inf bits order above every finite square)
+        bad |= rw_nonfinite(ss);
+#else
         bad |= rw_nonfinite(v[i].x) || rw_nonfinite(v[i].y) || rw_nonfinite(v[i].z) || rw_nonfinite(v[i].w);
+#endif
     }
     // whole-wave maximum (every lane holds its rows' pixel norms) and any-non-finite
 #pragma unroll
