@@ -20,8 +20,11 @@
 // * B fragment of (tap, row, half): lane l reads plane (part, l >> 4) at pixel (row + ky,
 //   16 half + (l & 15) + kx): one conflict-free ds_read_b128, a per-lane base plus an immediate;
 // * A fragments come straight from the F16 weight blob's [mtile][cblock16][tap][part][lane][8]
-//   layout (no new packing): lane l of quarter q reads 16 B at a per-lane offset, two half-taps
-//   (2 quarters each) ahead, from L2;
+//   layout (no new packing): lane l of quarter q reads 16 B at a per-lane offset, from L2 -- by
+//   default (h16_cblock12) a whole tap (4 quarters) one tap ahead, so each B fragment pair feeds 12
+//   MFMAs; h16_cblock (H16_B12=0, and the last layer with split outputs) works in half-taps
+//   (2 quarters each, 6 MFMAs per B pair) requested two half-taps ahead;
+// * layer 2 (FIRST): the stagers compute conv1 from the tile's image window in LDS;
 // * epilogue: a lane holds channels 16q + 4(l >> 4) .. +3 of pixel (l & 15): one dwordx4 store
 //   per (row, half, quarter); the c-block-major output [cblk16][h][w][16] is written as 1 KB
 //   runs; the last layer L2-normalises over the 4 lanes x 4 quarters that hold a pixel.
