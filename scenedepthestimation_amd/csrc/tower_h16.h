@@ -55,6 +55,14 @@ static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
 #ifndef H16_DIAG
 #define H16_DIAG 0
 #endif
+// Cache-policy bits of the stagers' activation loads: 1 (sc0) streams each activation past the CU's L1,
+// which leaves the L1 to the A fragments all four MFMA waves re-read every tap.  Timing builds showed the
+// MFMA waves waiting on those fragments (H16_DIAG 64: the same loads issued but not consumed runs 149 us
+// like no loads at all, 151, against 204 us).  Tower pair -8 to -30 us in three round-robin runs
+// (profiles/r05/tower_act_aux_nt.txt); 2 (nt) does not help; 0 = the default policy.
+#ifndef H16_ACT_AUX
+#define H16_ACT_AUX 1
+#endif
 
 // Split 4 channels, scaled by s, into the stage's (part, quarter) planes at dst (the unit's byte offset
 // in the stage, see h16_stager_loop).
@@ -123,12 +131,12 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
         if (ly >= XP_IY && lx >= XP_IX) {   // wave-uniform: the tile's input window is inside the input
 #pragma unroll
             for (int i = 0; i < XP_UPT; i++)
-                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, uoff[i], 0, 0));
+                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, uoff[i], 0, H16_ACT_AUX));
         } else {
 #pragma unroll
             for (int i = 0; i < XP_UPT; i++) {
                 const bool ok = (int)(uyx[i] >> 16) < ly && (int)(uyx[i] & 0xFFFFu) < lx;
-                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? uoff[i] : XP_OOB, 0, 0));
+                v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? uoff[i] : XP_OOB, 0, H16_ACT_AUX));
             }
         }
     };
@@ -451,7 +459,10 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
 #pragma unroll
         for (int hf = 0; hf < 2; hf++) {
             const int h = 2 * (s + 1) + hf;
-            if (!(H16_DIAG & 4))
+            if (H16_DIAG & 64) {   // timing probe: the loads issued into slots 1-3, the MFMAs on slot 0 only
+                abuf[1 + (2 * s + hf) % 3] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                                        : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+            } else if (!(H16_DIAG & 4))
                 abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
                                                 : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
         }
@@ -463,7 +474,7 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
             if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                const H16A &a = abuf[(H16_DIAG & 4) ? 0 : (2 * s + hf + PH) % 4];
+                const H16A &a = abuf[(H16_DIAG & (4 | 64)) ? 0 : (2 * s + hf + PH) % 4];
 #pragma unroll
                 for (int qq = 0; qq < 2; qq++) {
                     floatx4 &c = acc[rp * 4 + 2 * hf + qq];
