@@ -2,7 +2,7 @@
 """bench.py -- throughput of the stereo matching hot path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-                    [--workload north_star|cones|cv|c3|c4|c5|north_star_sgm]
+                    [--workload north_star|cones|cv|c3|c4|c5|north_star_sgm|cones_sgm]
                     [--mode auto|pairdp|dshard|dshard_rep|rowband] [--no-cpu-baseline] [--dump-disp PATH]
 
 A step = one stereo pair through the hot path with inputs resident in HBM:
@@ -12,8 +12,9 @@ accuracy) on both images -> fused certified cost volume + WTA over D disparities
 Default workload: the north-star size 1024x1024, D = 192 (BASELINE.json).
 
 N > 1 (one process per GPU under torchrun, RCCL).  The default --mode auto runs dshard (the north
-star's disparity-sharded cost volume) for `value` and times the other three schemes on the same pair
-after it (stages.multi_gpu_modes):
+star's disparity-sharded cost volume) for `value` on the tower + CV/WTA workloads and times the other
+three schemes on the same pair after it (stages.multi_gpu_modes); on the SGM workloads (c3,
+north_star_sgm: every SGM step needs all D) it runs pairdp:
   pairdp : every rank matches its own pair each step (config 4) -- weak scaling,
            no collective on the data path;
   dshard : one pair per step, disparity-sharded over the ranks with the feature
@@ -58,6 +59,8 @@ WORKLOADS = {
     "c3": (2000, 3000, 256, "tower+cbca+sgm"),
     # the north-star size through the reference's whole GPU path (+ the build-defined CBCA)
     "north_star_sgm": (1024, 1024, 192, "tower+cbca+sgm"),
+    # the cones pair through the same path (plumbing-size case of the SGM workloads)
+    "cones_sgm": (375, 450, 64, "tower+cbca+sgm"),
     # BASELINE config 4: Middlebury-2005/2006 scale pairs, one pair per GPU (pair-DP)
     "c4": (1110, 1390, 256, "tower+cv_wta"),
     # BASELINE config 5: one 4K pair, D = 512 (the fused CV+WTA never materialises the 17 GB volume, so
@@ -408,6 +411,19 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def resolve_mode(mode, world, what):
+    """--mode auto -> the scheme that runs: one GPU: the single-device hot path (pairdp); N > 1 on the
+    tower + CV/WTA workloads: north_star's disparity-sharded cost volume (dshard, strong scaling), with the
+    other schemes timed beside it in stages.multi_gpu_modes; the SGM workloads (every disparity per step)
+    run pair-DP replicas.  An explicit sharded mode on an SGM workload at N > 1 is refused."""
+    if mode == "auto":
+        return "dshard" if world > 1 and what == "tower+cv_wta" else "pairdp"
+    if world > 1 and what != "tower+cv_wta" and mode != "pairdp":
+        raise SystemExit(f"--mode {mode}: the sharded schemes run the tower + CV/WTA workloads only "
+                         f"(SGM needs every disparity per step: replicas only, --mode pairdp)")
+    return mode
+
+
 def make_mode(mode, H, W, D, what, rank, world, args, t_conv, t_cv, t_tower):
     """-> (step, pairs_per_step, scaling, parallelism, result): one multi-GPU scheme (or the single-device
     path, pairdp) on this rank.  The strong-scaling schemes match ONE pair (seed 0 on every rank); pair-DP
@@ -468,14 +484,7 @@ def main():
     # ranks sharing a GPU over gloo)
     H, W, D, what = WORKLOADS[args.workload]
     left, right, _ = stereo_pair(H, W, D, seed=rank)     # this rank's pair (pair-DP; rank 0: seed 0)
-    mode = args.mode
-    if mode == "auto":
-        # one GPU: the single-device hot path; N > 1: north_star's disparity-sharded cost volume
-        # (strong scaling), with the other schemes timed beside it in stages.multi_gpu_modes
-        mode = "pairdp" if world == 1 else "dshard"
-    if world > 1 and what != "tower+cv_wta" and mode != "pairdp":
-        raise SystemExit(f"--mode {mode}: the sharded schemes run the tower + CV/WTA workloads only "
-                         f"(SGM needs every disparity per step: replicas only, --mode pairdp)")
+    mode = resolve_mode(args.mode, world, what)
 
     t_conv, t_cv, t_tower = Timer(), Timer(), Timer()
     m = None
@@ -515,7 +524,7 @@ def main():
     disp_primary = result().detach().clone() if args.dump_disp else None
 
     multi = None
-    if world > 1 and args.mode == "auto":
+    if world > 1 and args.mode == "auto" and what == "tower+cv_wta":
         # the other multi-GPU schemes on the same pair, same ranks, same clock discipline (barrier +
         # max over ranks); pair-DP is weak scaling (world pairs per step), the rest strong (one pair)
         multi = {mode: {"ms_per_step": elapsed / args.steps * 1e3, "pairs_per_step": pairs_per_step,

@@ -168,8 +168,8 @@ int sde_set_persistent_grid(int cus);
  * [h][w][8 fp16] (256 B per pixel, as fp32 [h][w][64]), and publishes 2^sigma at out_absmax[32] (per image);
  * IN_SPLIT reads that layout and in_absmax[32] (LDS-DMA staging, no arithmetic).  2^sigma comes from an
  * a-priori bound of the outputs (max |b| + L1 * input bound, no fp16 overflow).  Layers >= 3 (IN) and
- * < nlayers (OUT), a layer between them with both or neither; at most 32 layers, fewer than 2^24 input pixels; bound-word arrays of >= 33 words per
- * image; not with the CBLOCK flag of the same side, WINOGRAD or MFMA32. */
+ * < nlayers (OUT), a layer between them with both or neither; at most 32 layers, fewer than 2^24 input pixels; bound-word arrays extending >= 33 words past
+ * the word passed (batches: amax_stride >= 64 words per image, so no image's scale word lands on the next image's row); not with the CBLOCK flag of the same side, WINOGRAD or MFMA32. */
 #define SDE_TOWER_IN_SPLIT 64
 #define SDE_TOWER_OUT_SPLIT 128
 

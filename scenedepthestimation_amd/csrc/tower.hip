@@ -1133,7 +1133,12 @@ __global__ __launch_bounds__(512) void conv64_x6p_kernel(const float *__restrict
 
 }  // namespace sde
 #include "tower_wino.h"
+// A/B timing builds substitute a probe copy of this header (tools/build_file_variant.sh -DSDE_H16_HEADER=...)
+#ifdef SDE_H16_HEADER
+#include SDE_H16_HEADER
+#else
 #include "tower_h16.h"
+#endif
 #include "tower_h16q.h"
 #ifndef SDE_H16_L2
 #define SDE_H16_L2 1   // 0: layer 2 on conv64_x6p_kernel (32x32x16), for A/B builds
@@ -1833,8 +1838,10 @@ SDE_EXPORT int sde_tower_layer_batch(const float *in, int nimg, int64_t in_strid
     if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax) || (nimg > 1 && amax_stride < 1)))
         return SDE_ERR_ARG;
     const bool in_sp = (flags & SDE_TOWER_IN_SPLIT) != 0, out_sp = (flags & SDE_TOWER_OUT_SPLIT) != 0;
+    // split activations: a layer's scale word sits 32 words past its bound word, which is column <= 31 of the
+    // image's row; rows of fewer than 64 words would put image i's scale word on image i + 1's bound words
     if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, (int64_t)Hin * Win) ||
-        ((in_sp || out_sp) && nimg > 1 && amax_stride <= XP_SCALE_WORD))
+        ((in_sp || out_sp) && nimg > 1 && amax_stride < (int)(TOWER_AMAX_BYTES / sizeof(float))))
         return SDE_ERR_ARG;
     launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, nullptr, nullptr, nullptr, in_cb, out_cb,
                  in_absmax, out_absmax, as_stream(stream), nimg, in_stride, out_stride, amax_stride, in_sp, out_sp);

@@ -479,7 +479,11 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
                 // count of stores per wave for the next pass's vmcnt wait
                 const uint32_t off = OUT_CB ? (((uint32_t)(c0 >> 4) * Hout + y) * Wout + ox) * 64u + 4u * (c0 & 15)
                                             : ((uint32_t)y * Wout + ox) * 256u + 4u * c0;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), orsrc, ok ? off : WN_OOB, 0, 0);
+                const u32x4 od = __builtin_bit_cast(u32x4, o);
+                __builtin_amdgcn_raw_buffer_store_b128(od, orsrc, ok ? off : WN_OOB, 0, 0);
+                // the store's data registers stay untouched for >= 9 wait states ("store-data
+                // overwrite"; _isa_lint.MFMA_STORE_DATA_WINDOW)
+                asm volatile("s_nop 7\n\ts_nop 1" ::"v"(od));
             }
             __builtin_amdgcn_s_waitcnt(WN_LGKM0);
             __builtin_amdgcn_s_barrier();     // the P reads are done before P (or a stage) is rewritten
@@ -496,10 +500,11 @@ __global__ __launch_bounds__(512) void wino_kernel(const float *__restrict__ in,
                 const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
                 const int y = oy + i;
                 const uint32_t off = y < Hout && ox < Wout ? ((uint32_t)y * Wout + ox) * 256u + 16u * fq : WN_OOB;
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(u32x4, make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv)), orsrc, off, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(u32x4, make_float4(b.x * inv, b.y * inv, b.z * inv, b.w * inv)), orsrc, off + 128u, 0, 0);
+                const u32x4 oa = __builtin_bit_cast(u32x4, make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv));
+                const u32x4 ob = __builtin_bit_cast(u32x4, make_float4(b.x * inv, b.y * inv, b.z * inv, b.w * inv));
+                __builtin_amdgcn_raw_buffer_store_b128(oa, orsrc, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(ob, orsrc, off + 128u, 0, 0);
+                asm volatile("s_nop 7\n\ts_nop 1" ::"v"(oa), "v"(ob));   // >= 9 wait states, as above
             }
         } else {
             // the bound word of an image: one atomic per wave and image (a flush when the passes move

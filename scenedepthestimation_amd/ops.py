@@ -329,6 +329,7 @@ def absmax_batch(x, out):
 
 
 SCALE_WORD = 32   # split activations: 2^sigma at bound word + 32 (sde.h SDE_TOWER_OUT_SPLIT)
+AMAX_ROW_WORDS = 64   # a batch's bound-word row per image (tower.hip TOWER_AMAX_BYTES / 4)
 # whether sde_tower_forward* pass split activations between the default f16x3 tower's 64->64 layers
 # (tower.hip SDE_SPLIT_ACT; the layer-by-layer drivers in pipeline.py follow it to stay bit-identical)
 TOWER_SPLIT_ACT = False
@@ -402,6 +403,12 @@ def tower_layer_batch(inp, packed, nlayers: int, layer: int, out, nf: int = 64, 
         _check_scale_word(in_absmax, N, "in_absmax")
     if out_split:
         _check_scale_word(out_absmax, N, "out_absmax")
+    if (in_split or out_split) and N > 1:
+        for words, name in ((in_absmax, "in_absmax"), (out_absmax, "out_absmax")):
+            if words is not None and words.stride(0) < AMAX_ROW_WORDS:
+                raise ValueError(f"{name}: split activations over a batch need rows of >= {AMAX_ROW_WORDS} bound words "
+                                 f"(got a row stride of {words.stride(0)}): a layer's scale word is {SCALE_WORD} "
+                                 "words past its bound word")
     sh = 4 if layer == 2 else 2
     oshape = (N, Hin - sh, Win - sh, nf)
     ws = 0

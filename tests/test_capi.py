@@ -140,6 +140,11 @@ def test_argument_validation_without_gpu():
     assert scaled(3, 8 | 64 | 128 | 2) == ERR           # IN_SPLIT with IN_CBLOCK
     assert scaled(3, 8 | 64 | 128 | 32) == ERR          # with the 32x32x16 kernel
     assert scaled(3, 8 | 64 | 128, L=33) == ERR         # the scale word needs <= 32 layers
+    # split activations over a batch: image i's scale word (bound word + 32) must not reach image i + 1's row
+    batch = lambda stride: lib.sde_tower_layer_batch(1, 2, 8 * 8 * 64, 8, 8, 1, 5, 64, 3, 1, 6 * 6 * 64,
+                                                     8 | 64 | 128, 1, 1, stride, N)
+    for stride in (33, 34, 35, 63):
+        assert batch(stride) == ERR, stride
     assert lib.sde_absmax_f32(N, 4, 1, N) == ERR
     assert lib.sde_feature_split(1, 10, 32, 1, 1, 1, N) == ERR                                     # C != 64
     assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace
@@ -201,6 +206,19 @@ def test_isa_lint_flags_store_data_overwrite():
     assert _isa_lint.lint_text(nop) == []
     assert _isa_lint.lint_text(far) == []
     assert _isa_lint.lint_text(other) == []
+    # kernels with MFMAs: a write is flagged until MFMA_STORE_DATA_WINDOW (9) wait states have passed;
+    # AGPR store data is tracked like VGPR data
+    mf = "\tv_mfma_f32_16x16x32_f16 v[0:3], v[4:7], v[8:11], v[0:3]\n"
+    far_mfma = head + mf + ("\tbuffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen\n"
+                            "\ts_nop 4\n\tv_max_u32_e32 v180, v176, v177\n")
+    ok_mfma = head + mf + ("\tbuffer_store_dwordx4 v[180:183], v206, s[28:31], s68 offen\n"
+                           "\ts_nop 7\n\ts_nop 0\n\tv_max_u32_e32 v180, v176, v177\n")
+    agpr = head + mf + ("\tglobal_store_dwordx4 v[0:1], a[4:7], off\n\tv_accvgpr_write_b32 a6, v2\n")
+    assert len(_isa_lint.lint_text(far_mfma)) == 1 and _isa_lint.lint_text(far) == []
+    assert _isa_lint.lint_text(ok_mfma) == []
+    assert len(_isa_lint.lint_text(agpr)) == 1
+    # one function's MFMAs do not widen the window of the next one
+    assert _isa_lint.lint_text(head + mf + "0000000000002000 <k2>:\n" + far.split("\n", 1)[1]) == []
 
 
 def test_isa_lint_passes_on_the_built_library():

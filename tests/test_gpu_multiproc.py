@@ -101,3 +101,43 @@ def test_bench_multirank_modes_on_one_gpu(gpu, tmp_path, mode, primary, scaling)
             assert np.array_equal(np.load(f"{dump}.{om}.npy"), want), f"{om}: map differs from the single-device one"
     del m
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_bench_multirank_sgm_workload_default_mode(gpu, tmp_path):
+    """bench.py --gpus 2 on an SGM workload with no --mode flag: auto resolves to pair-DP
+    replicas (SGM needs every disparity per step), one JSON line, and rank 0's map equals the
+    single-device whole GPU path's."""
+    import json
+
+    import numpy as np
+    import torch
+
+    import bench
+    from scenedepthestimation_amd.pipeline import StereoMatcher
+    from scenedepthestimation_amd.synthetic import stereo_pair
+    port = _free_port()
+    env = dict(os.environ, SDE_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dump = str(tmp_path / "disp.npy")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--workload", "cones_sgm", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dump-disp", dump]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    if p.returncode != 0:
+        print(p.stdout[-3000:], "\n---- stderr ----\n", "\n".join(l for l in p.stderr.splitlines() if "Gloo" not in l)[-6000:])
+    assert p.returncode == 0, "bench.py --gpus 2 --workload cones_sgm failed (output above)"
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["config"]["parallelism"] == "pairdp2"
+    assert line["value"] > 0 and "multi_gpu_modes" not in line.get("stages", {})
+    H, W, D, _ = bench.WORKLOADS["cones_sgm"]
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    m = StereoMatcher(H, W, D, sgm=True, cbca_iters=bench.CBCA_ITERS, cbca_L1=bench.CBCA_L1, cbca_tau=bench.CBCA_TAU)
+    m.load_images(left, right)
+    m.features()
+    m.sgm_path(post=True)
+    want = m.sgm_bufs["disp"][0].cpu().numpy()
+    assert np.array_equal(np.load(dump), want), "pairdp SGM map differs from the single-device one"
+    del m
+    torch.cuda.empty_cache()

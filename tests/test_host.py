@@ -120,3 +120,35 @@ def test_cli_normalise_is_reference_numpy():
     x = normalise(img)
     ref = (img - np.mean(img, axis=(0, 1))) / np.std(img, axis=(0, 1))
     assert x.shape == (9, 11, 1) and x[..., 0].tobytes() == ref.tobytes()
+
+
+def test_bench_mode_resolution():
+    """bench.py --mode auto: dshard only where the sharded schemes apply (tower + CV/WTA at
+    N > 1); the SGM workloads and one GPU run pair-DP; an explicit sharded mode on an SGM workload at N > 1
+    is refused, at N = 1 it is the single-device path."""
+    import bench
+    assert bench.resolve_mode("auto", 1, "tower+cv_wta") == "pairdp"
+    assert bench.resolve_mode("auto", 8, "tower+cv_wta") == "dshard"
+    for w in ("c3", "north_star_sgm", "cones_sgm"):
+        what = bench.WORKLOADS[w][3]
+        assert bench.resolve_mode("auto", 8, what) == "pairdp"
+        assert bench.resolve_mode("auto", 1, what) == "pairdp"
+        with pytest.raises(SystemExit):
+            bench.resolve_mode("dshard", 2, what)
+    assert bench.resolve_mode("rowband", 4, "tower+cv_wta") == "rowband"
+
+
+def test_split_batch_bound_rows_checked():
+    """ops.tower_layer_batch refuses split activations over a batch whose bound-word rows are shorter than
+    64 words (the scale word, 32 words past a layer's bound word, would land on the next image's
+    row) before anything touches a device."""
+    import torch
+
+    from scenedepthestimation_amd import ops
+    x = torch.zeros((2, 8, 8, 64))
+    y = torch.zeros((2, 6, 6, 64))
+    for stride in (33, 35, 63):
+        words = torch.zeros(2 * stride + 64)[:2 * stride].view(2, stride)   # room for every scale word
+        with pytest.raises(ValueError, match="rows of >= 64"):
+            ops.tower_layer_batch(x, None, 5, 3, y, in_absmax=words, out_absmax=words[:, 1:], in_split=True,
+                                  out_split=True)

@@ -1,5 +1,5 @@
 """Phase breakdown of the certified CV+WTA's compute waves (timing-only build: tools/_var/libsde_cvdiag.so,
-bash tools/build_file_variant.sh cv_row.hip cvdiag -DCV_DIAG=1).  Wave 0 of each workgroup sums s_memtime
+SRC=tools/variants/cv_row_diag.hip bash tools/build_file_variant.sh cv_row.hip cvdiag -DCV_DIAG=1).  Wave 0 of each workgroup sums s_memtime
 deltas per superstrip phase: 0 = left split (+ next left load issue), 1 = tile sweep (MFMAs + scores),
 2 = merges, 3 = the superstrip barrier, 4 = epilogue stores; plus the whole loop in s_memtime and in
 s_memrealtime (100 MHz) ticks.  Printed: median over workgroups, cycles per superstrip, and the clock.

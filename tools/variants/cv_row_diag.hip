@@ -1,3 +1,6 @@
+// cv_row_diag.hip -- PROBE COPY of scenedepthestimation_amd/csrc/cv_row.hip with the CV_DIAG phase stamps
+// (timing-only, wrong outputs).  Build: SRC=tools/variants/cv_row_diag.hip bash tools/build_file_variant.sh
+// cv_row.hip cvdiag -DCV_DIAG=1 (tools/cv_diag.py).  Never part of libsde.so.
 // cv_row.hip -- row-sweep certified fused cost volume + WTA (north-star kernel).
 //
 // Replaces (WHDY/SceneDepthEstimation) compute_cost_volume + WTA1,
@@ -328,6 +331,9 @@ constexpr int R2_NX = 128;                 // left pixels per superstrip (4 comp
 #define CV_FASTSPLIT 31                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle,
                                            // 16 the stagers' flag from the pixel norm (A/B builds)
 #endif
+#ifndef CV_DIAG
+#define CV_DIAG 0                          // timing-only builds (tools/cv_diag.py): phase stamps, wrong outputs
+#endif
 constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
 
 // one stager lane's 8 units (pixel u >> 4, channels 4 (u & 15) ..) of right tile T: unit u = lane + 64 i
@@ -442,6 +448,14 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
     };
     load_left(0);
     __syncthreads();
+#if CV_DIAG
+    // timing-only builds: wave 0's s_memtime deltas per superstrip phase, summed, to out_disp[8 b ..]
+    uint64_t dg[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime();
+    const uint64_t tstart = tp, rstart = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&](int i) { const uint64_t t = __builtin_amdgcn_s_memtime(); dg[i] += t - tp; tp = t; };
+#else
+    auto stamp = [&](int) {};
+#endif
 
     for (int k = 0; k < nss; k++) {
         const int tlo = tlo0 + R2_NEW * k;
@@ -518,6 +532,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
 #endif
             nl = sqrtf(ssl) * FX_NORM_UP;
             if (more) load_left(k + 1);
+            stamp(0);
 
             float b1[4], b2[4];
             int ag[4];
@@ -634,6 +649,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     }
                 }
             }
+            stamp(1);
             // a chain that took a score holds d + t >= t >= 0; one that took none still holds -1
 #pragma unroll
             for (int t = 0; t < 4; t++) ag[t] = ag[t] >= 0 ? ag[t] - t : -1;
@@ -653,9 +669,11 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 fx_merge(best, arg, second, bb, aa, ss2);
             }
         }
+        stamp(2);
         // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
         // barrier per superstrip orders both directions
         __syncthreads();
+        stamp(3);
         if (xb < W && h == 0 && xok) {
             const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
             const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
@@ -674,7 +692,17 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 list[atomicAdd(counter, 1u)] = (int32_t)p;
             }
         }
+        stamp(4);
     }
+#if CV_DIAG
+    __syncthreads();   // every pixel's output stored: the stamps overwrite out_disp[8 b .. 8 b + 7] after them
+    if (wave == 0 && lane == 0 && out_disp) {
+        for (int i = 0; i < 5; i++) out_disp[8 * (size_t)blockIdx.x + i] = (float)dg[i];
+        out_disp[8 * (size_t)blockIdx.x + 5] = (float)(__builtin_amdgcn_s_memtime() - tstart);
+        out_disp[8 * (size_t)blockIdx.x + 6] = (float)(__builtin_amdgcn_s_memrealtime() - rstart);
+        out_disp[8 * (size_t)blockIdx.x + 7] = (float)nss;
+    }
+#endif
 }
 
 // tiles spanned by a superstrip's window and the first one (superstrip 0), floor division

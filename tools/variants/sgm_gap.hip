@@ -1,3 +1,6 @@
+// sgm_gap.hip -- PROBE COPY of scenedepthestimation_amd/csrc/sgm.hip with the SGM_GAP switch (what sits between
+// two passes of the pair; tools/sgm_gap_probe.py).  Build: SRC=tools/variants/sgm_gap.hip bash
+// tools/build_file_variant.sh sgm.hip sgmgapN -DSGM_GAP=N.  Never part of libsde.so.
 // sgm.hip -- semi-global matching and the GPU path's post-processing (gfx950).
 //
 // Replaces (process_functional.py):
@@ -1247,6 +1250,19 @@ static int sgm_pair(const float *cv_l, const float *pen_l, float *S_l, float *di
                                          dir == 0 && fold_du,
                                          wta && dir == 7);
         if (s != SDE_OK) return s;
+#ifdef SGM_GAP
+        // probe builds (tools/sgm_gap_probe.py): what sits between two passes of the pair
+        if (dir < 7) {
+            if (SGM_GAP == 1) (void)hipStreamSynchronize(st);
+            if (SGM_GAP == 2 || SGM_GAP == 3) {
+                // 2: an event created with a system-scope release (L2 written back at the record)
+                static hipEvent_t ev = nullptr;
+                if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming |
+                                                                 (SGM_GAP == 2 ? hipEventReleaseToSystem : 0));
+                (void)hipEventRecord(ev, st);
+            }
+        }
+#endif
     }
     return launch_status();
 }

@@ -1,3 +1,7 @@
+// tower_h16_diag.h -- PROBE COPY of scenedepthestimation_amd/csrc/tower_h16.h for timing-only builds (wrong results
+// under any nonzero H16_DIAG / H16_ACC16); built by tools/build_file_variant.sh tower.hip NAME
+// -DSDE_H16_HEADER='"<abs path of this file>"' -DH16_DIAG=n.  Never part of libsde.so.
+//
 // tower_h16.h -- the MC-CNN tower's 64 -> 64 layers (3..L; mc_cnn_brunch.py:31-48, conv :70-92) as
 // a direct 3x3 implicit GEMM on v_mfma_f32_16x16x32_f16 (included by tower.hip; f16x3 arithmetic).
 //
@@ -47,14 +51,34 @@ static_assert(H16_SMEM <= 163840, "LDS");
 constexpr size_t H16_WIN_OFF = H16_SMEM;
 constexpr size_t H16_SMEM_FIRST = H16_WIN_OFF + XP_WIN * sizeof(float);   // 162,880 B
 static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
-// Timing-only diagnostic builds (no epilogue stores, no stager work, constant A or B operands, in-kernel
-// clock stamps, ring-depth probes; wrong results) live in the probe copy tools/variants/tower_h16_diag.h,
-// which tools/build_file_variant.sh substitutes for this header (-DSDE_H16_HEADER=...).
+// Timing-only diagnostic builds (tools/build_file_variant.sh tower.hip NAME -DH16_DIAG=n; wrong results):
+// 1 = no epilogue stores, 2 = stagers skip their loads and splits, 4 = MFMA waves reuse one A fragment
+// set (no A loads in the loop), 8 = wave 0 of each workgroup writes its (s_memtime, s_memrealtime) deltas
+// over the kernel as two floats to out[2 * blockIdx.x ..] at the end (in-kernel clock, tools/tower_variants.py).
+// 0 (the product) = everything.
+#ifndef H16_DIAG
+#define H16_DIAG 0
+#endif
 // Cache-policy bits of the stagers' activation loads: 1 (sc0) streams each activation past the CU's L1,
 // which leaves the L1 to the A fragments all four MFMA waves re-read every tap.  Timing builds showed the
-// MFMA waves waiting on those fragments (a probe build with the same loads issued but not consumed runs 149 us
+// MFMA waves waiting on those fragments (H16_DIAG 64: the same loads issued but not consumed runs 149 us
 // like no loads at all, 151, against 204 us).  Tower pair -8 to -30 us in three round-robin runs
 // (profiles/r05/tower_act_aux_nt.txt); 2 (nt) does not help; 0 = the default policy.
+// 128-free probes: H16_ACC16 = 1 folds a wave's rows 2, 3 onto rows 0, 1 (16 accumulators, 64 VGPRs freed; the
+// same MFMAs, B reads and stores); H16_RING = T: the B12 c-block's A ring holds T taps (requested T - 1 taps ahead).
+#ifndef H16_ACC16
+#define H16_ACC16 0
+#endif
+#ifndef H16_RING
+#define H16_RING 2
+#endif
+#ifndef H16_AREAL
+#define H16_AREAL 1
+#endif
+#ifndef H16_ORDER
+#define H16_ORDER 0
+#endif
+#define H16_AR(rp) (H16_ACC16 ? ((rp) & 3) : (rp))
 #ifndef H16_ACT_AUX
 #define H16_ACT_AUX 1
 #endif
@@ -150,6 +174,12 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
             if (h16_unit(st, i) < XP_UNITS) h16_put(sb + ulds[i], v[i], s);
     };
     float4 ra[XP_UPT], rb[XP_UPT];
+    if (H16_DIAG & 2) {
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < nsteps; i++) __syncthreads();
+        return;
+    }
     load(ra, 0);
     load(rb, 1);
     store(ra, 0);
@@ -297,7 +327,8 @@ __device__ __forceinline__ void h16_dma_stager_loop(char *hsm, const float *__re
 #pragma unroll
     for (int d = 0; d < ND; d++) {
         const int px = d * 64 + lane, iy = px / XP_IX, ix = px - iy * XP_IX;
-        voff[d] = (uint32_t)((iy * Win + ix) * 16);
+        voff[d] = (H16_DIAG & 32) ? (uint32_t)(((iy * (Win / 32) + (ix >> 5)) * 16) * 512 + (ix & 31) * 16)
+                                  : (uint32_t)((iy * Win + ix) * 16);
     }
     const size_t PB = (size_t)Hin * Win * 16;
     auto issue = [&](int k) {
@@ -310,7 +341,11 @@ __device__ __forceinline__ void h16_dma_stager_loop(char *hsm, const float *__re
 #pragma unroll
         for (int pp = 0; pp < 2; pp++) {
             const int p = 2 * w + pp;
-            const __amdgpu_buffer_rsrc_t rs = xp_rsrc_n(src + p * PB, (uint32_t)(PB - org));
+            __amdgpu_buffer_rsrc_t rs = xp_rsrc_n(src + p * PB, (uint32_t)(PB - org));
+            if (H16_DIAG & 32) {   // timing probe: blocked layout [h][w / 32][16 planes][32][16 B]
+                const size_t o2 = ((size_t)(ty0 * (Win / 32) + (tx0 >> 5)) * 16 + cb * 8 + p) * 512;
+                rs = xp_rsrc_n(reinterpret_cast<const char *>(in + img * bt.in_stride) + o2, (uint32_t)(16 * PB - o2));
+            }
             auto *lds = (__attribute__((address_space(3))) char *)(dst + p * H16_PLANE);
 #pragma unroll
             for (int d = 0; d < ND - 1; d++)
@@ -318,6 +353,12 @@ __device__ __forceinline__ void h16_dma_stager_loop(char *hsm, const float *__re
             if (lane < NLAST) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds + (ND - 1) * 1024, 16, voff[ND - 1], 0, 0, 0);
         }
     };
+    if (H16_DIAG & 2) {
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < nsteps; i++) __syncthreads();
+        return;
+    }
     issue(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -346,7 +387,11 @@ __device__ __forceinline__ H16A h16_afrag(__amdgpu_buffer_rsrc_t ra, uint32_t vo
     for (int p = 0; p < 2; p++)
 #pragma unroll
         for (int qq = 0; qq < 2; qq++) {
-            const int k = (((hf * XP_NCB * 9 + tap) * 2 + p) * 64 + 16 * qq) * 16;
+            // 1024: only MFMA waves < H16_AREAL load real A fragments, the others the same (L1-resident) bytes every
+            // tap: the CU's L2 A traffic scaled by H16_AREAL / 4 at the same instruction count
+            const bool real = !(H16_DIAG & 1024) || (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < H16_AREAL;
+            const int kc = (p * 64 + 16 * qq) * 16;
+            const int k = (H16_DIAG & 256) ? kc : real ? ((((hf * XP_NCB * 9 + tap) * 2 + p) * 64 + 16 * qq) * 16) : kc;
             a.f[p][qq] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, cbo + k, 0));
         }
     return a;
@@ -388,9 +433,10 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[NA],
     for (int k = 0; k < H16_RD - 1; k++) ring[k] = h16_bfrag(sb, k);
 #pragma unroll
     for (int s = 0; s < H16_HT; s++) {
-        abuf[(s + 2) % 3] = s + 2 < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, s + 2)
-                                           : h16_afrag(ra, avoff, ncb * H16_A_CB, s + 2 - H16_HT);
-        const H16A &a = abuf[s % 3];
+        if (!(H16_DIAG & 4))
+            abuf[(s + 2) % 3] = s + 2 < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, s + 2)
+                                               : h16_afrag(ra, avoff, ncb * H16_A_CB, s + 2 - H16_HT);
+        const H16A &a = abuf[(H16_DIAG & 4) ? 0 : s % 3];
         const int hf = s & 1;
 #pragma unroll
         for (int rp = 0; rp < 8; rp++) {
@@ -417,7 +463,7 @@ __device__ __forceinline__ void h16_cblock(floatx4 (&acc)[32], H16A (&abuf)[NA],
 __device__ __forceinline__ H16B h16_bfrag12(const char *sb, int b)
 {
     const int tap = b >> 3, r = (b >> 1) & 3, ph = b & 1;
-    const int off = ((r + tap / 3) * XP_IX + 16 * ph + tap % 3) * 16;
+    const int off = (H16_DIAG & 512) ? (b & 1) * 16 : ((r + tap / 3) * XP_IX + 16 * ph + tap % 3) * 16;
     H16B f;
     f.hi = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + off));
     f.lo = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4 *>(sb + 4 * H16_PLANE + off));
@@ -436,8 +482,65 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
 #pragma unroll
         for (int hf = 0; hf < 2; hf++) {
             const int h = 2 * (s + 1) + hf;
-            abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
-                                            : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+            if (H16_DIAG & 64) {   // timing probe: the loads issued into slots 1-3, the MFMAs on slot 0 only
+                abuf[1 + (2 * s + hf) % 3] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                                        : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+            } else if (!(H16_DIAG & 4))
+                abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                                : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+        }
+#pragma unroll
+        for (int rp = 0; rp < 8; rp++) {
+            const int b = s * 8 + rp;
+            __builtin_amdgcn_sched_barrier(0);
+            const H16B &bf = ring[b & 1];
+            if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
+            if (H16_ORDER == 1) {   // probe: B-major order (each accumulator's three products in the same order)
+#pragma unroll
+                for (int pp = 0; pp < 3; pp++)
+#pragma unroll
+                    for (int hf = 0; hf < 2; hf++) {
+                        const H16A &a = abuf[(H16_DIAG & (4 | 64)) ? 0 : (2 * s + hf + PH) % 4];
+#pragma unroll
+                        for (int qq = 0; qq < 2; qq++) {
+                            floatx4 &c = acc[H16_AR(rp) * 4 + 2 * hf + qq];
+                            c = mfma16(a.f[pp == 0 ? 1 : 0][qq], pp == 1 ? bf.lo : bf.hi, c);
+                        }
+                    }
+            } else {
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                const H16A &a = abuf[(H16_DIAG & (4 | 64)) ? 0 : (2 * s + hf + PH) % 4];
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) {
+                    floatx4 &c = acc[H16_AR(rp) * 4 + 2 * hf + qq];
+                    c = mfma16(a.f[1][qq], bf.hi, c);
+                    c = mfma16(a.f[0][qq], bf.lo, c);
+                    c = mfma16(a.f[0][qq], bf.hi, c);
+                }
+            }
+            }
+        }
+    }
+}
+
+// Probe: the B12 c-block with a T-tap A ring (tap s requests tap s + T - 1 into the slots tap s - 1 left); 18 half-taps
+// per c-block, so T = 3 keeps every c-block in phase 0.
+template <int T>
+__device__ __forceinline__ void h16_cblock12r(floatx4 (&acc)[32], H16A (&abuf)[2 * T], __amdgpu_buffer_rsrc_t ra,
+                                              uint32_t avoff, int cb, int ncb, const char *sb)
+{
+    static_assert(H16_HT % (2 * T) == 0, "ring phase");
+    constexpr int NT = 9, NB = NT * 8;
+    H16B ring[2];
+    ring[0] = h16_bfrag12(sb, 0);
+#pragma unroll
+    for (int s = 0; s < NT; s++) {
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) {
+            const int h = 2 * (s + T - 1) + hf;
+            abuf[h % (2 * T)] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                           : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
         }
 #pragma unroll
         for (int rp = 0; rp < 8; rp++) {
@@ -447,10 +550,10 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
             if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                const H16A &a = abuf[(2 * s + hf + PH) % 4];
+                const H16A &a = abuf[(2 * s + hf) % (2 * T)];
 #pragma unroll
                 for (int qq = 0; qq < 2; qq++) {
-                    floatx4 &c = acc[rp * 4 + 2 * hf + qq];
+                    floatx4 &c = acc[H16_AR(rp) * 4 + 2 * hf + qq];
                     c = mfma16(a.f[1][qq], bf.hi, c);
                     c = mfma16(a.f[0][qq], bf.lo, c);
                     c = mfma16(a.f[0][qq], bf.hi, c);
@@ -509,7 +612,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                 for (int ph = 0; ph < 2; ph++) {
                     const int x = tx0 + 16 * ph + j;
                     const bool xok = x < Wout;
-                    const floatx4 &c = acc[(r * 2 + ph) * 4 + q];
+                    const floatx4 &c = acc[(H16_AR(r * 2) + ph) * 4 + q];
                     float o4[4];
                     // OSPL: the outputs scaled by 2^sigma straight from the accumulators (scale folded into
                     // the unscale and the bias: exact), their bound unscaled below
@@ -530,7 +633,14 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                             }
                             const uint32_t v2 = xok ? ospl_lane + (uint32_t)x * 16u : XP_OOB;
                             const uint32_t s2 = (uint32_t)((row0 + r) * Wout) * 16u;
-                            __builtin_amdgcn_raw_buffer_store_b128(v4, rs, v2, s2, 0);
+                            if (H16_DIAG & 16) {   // timing probe: blocked layout (last partial block column skipped)
+                                if (tx0 + 32 <= Wout) {
+                                    const int P = (q >> 1) * 8 + 2 * (q & 1) + (k4 & 1) * 4 + (k4 >> 1);
+                                    const uint32_t a = (uint32_t)((((ty0 + row0 + r) * (Wout / 32) + (tx0 >> 5)) * 16 + P) * 512 +
+                                                                  (16 * ph + j) * 16);
+                                    __builtin_amdgcn_raw_buffer_store_b128(v4, xp_rsrc(outi), a, 0, 0);
+                                }
+                            } else if (!(H16_DIAG & 1)) __builtin_amdgcn_raw_buffer_store_b128(v4, rs, v2, s2, 0);
                         }
                     } else {
                         pin[k] = __builtin_bit_cast(u32x4, o);
@@ -539,7 +649,8 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                                 amax = max(amax, max(__float_as_uint(o.x), __float_as_uint(o.y)));
                                 amax = max(amax, max(__float_as_uint(o.z), __float_as_uint(o.w)));
                             }
-                            xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB, so);
+                            if (!(H16_DIAG & 1)) xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB,
+                                   so);
                         }
                     }
                     if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
@@ -671,10 +782,20 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     // c-blocks feeding each B fragment to all four quarters (h16_cblock12), except the last layer with
     // split outputs (its epilogue would spill 13 VGPRs with the 2-tap A ring)
     constexpr bool B12 = H16_B12 == 2 ? !(LAST && SPLIT) : H16_B12 == 1 ? !LAST && !FIRST : false;
-    H16A abuf[4];   // h16_cblock: slots 0-2
+    constexpr bool RING = B12 && H16_RING == 3;
+    H16A abuf[RING ? 6 : 4];   // h16_cblock: slots 0-2
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
+    if constexpr (RING) {
+        abuf[2] = h16_afrag(ra, avoff, 0, 2);
+        abuf[3] = h16_afrag(ra, avoff, 0, 3);
+    }
     __syncthreads();
+    uint64_t clk0 = 0, rt0 = 0;
+    if (H16_DIAG & 8) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
 
     int sc_img = -1;
     float sc_u = 1.0f, sc_o = 1.0f;
@@ -689,7 +810,9 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         for (int i = 0; i < 32; i++) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
         // cb 0, then cb 1 and the epilogue (as a lambda: B12 unrolls the pair, the 3-slot form keeps a loop)
         auto cstep = [&](int cb) {
-            if constexpr (B12) {
+            if constexpr (RING) {
+                h16_cblock12r<3>(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
+            } else if constexpr (B12) {
                 if (cb == 0) h16_cblock12<0>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
                 else h16_cblock12<2>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
             } else {
@@ -722,6 +845,11 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         }
     }
     if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+    if ((H16_DIAG & 8) && wave == 0 && lane == 0) {
+        const uint64_t c = __builtin_amdgcn_s_memtime() - clk0, r = __builtin_amdgcn_s_memrealtime() - rt0;
+        out[2 * blockIdx.x] = (float)c;
+        out[2 * blockIdx.x + 1] = (float)r;
+    }
 }
 
 }  // namespace sde
