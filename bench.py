@@ -424,6 +424,37 @@ def resolve_mode(mode, world, what):
     return mode
 
 
+def c3_stage(args, steps=3):
+    """BASELINE config 3 on the north-star line: the 2000x3000 pair at D = 256 through
+    tower x2 + L volume + CBCA x2 (sde_cbca_lr) + SGM both sides + WTA + LR check / LRC / median
+    (disparity_compute_by_gpu, process_functional.py:1093-1267), `steps` timed steps after one warm-up with
+    the barrier-free single-GPU clock of the main line (synchronise, wall clock, synchronise), plus the per-kernel
+    HBM fractions of gpu_path_stages.  No CPU leg."""
+    H, W, D, what = WORKLOADS["c3"]
+    m = StereoMatcher(H, W, D, tower_precision=args.tower_precision, sgm=True, cbca_iters=CBCA_ITERS,
+                      cbca_L1=CBCA_L1, cbca_tau=CBCA_TAU)
+    left, right, _ = stereo_pair(H, W, D, seed=0)
+    m.load_images(left, right)
+    t = Timer()
+    step = make_step(m, what, t, t, t)
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    vox = float(H) * W * D
+    out = {"workload": "c3", "H": H, "W": W, "D": D, "steps": steps, "ms_per_pair": el / steps * 1e3,
+           "Mvox_s": vox * steps / el / 1e6,
+           "pipeline": "u8 pair -> preprocess -> tower x2 -> L volume -> CBCA x2 (+ shear) -> SGM both sides + WTA "
+                       "-> LR check / LRC / median"}
+    out.update(gpu_path_stages(m))
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
 def make_mode(mode, H, W, D, what, rank, world, args, t_conv, t_cv, t_tower):
     """-> (step, pairs_per_step, scaling, parallelism, result): one multi-GPU scheme (or the single-device
     path, pairdp) on this rank.  The strong-scaling schemes match ONE pair (seed 0 on every rank); pair-DP
@@ -473,6 +504,8 @@ def main():
     ap.add_argument("--dump-disp", default=None, help="rank 0 saves the disparity map (.npy; auto mode: also "
                                                          "<path>.<mode>.npy for every other scheme)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true", help="north_star: skip stages.c3 (BASELINE config 3 timed "
+                                                         "beside the line)")
     ap.add_argument("--tower-precision", default="f16x3", choices=["fp32", "bf16x6", "f16x3", "f16x3w", "f16x3m32"])
     ap.add_argument("--cv-mode", default="certified", choices=["certified", "exact"])
     args = ap.parse_args()
@@ -673,6 +706,8 @@ def main():
                 stages["reference_gpu_path"] = gpu_path_stages(ms_)
                 del ms_
                 torch.cuda.empty_cache()
+            if args.workload == "north_star" and world == 1 and not args.no_c3:
+                stages["c3"] = c3_stage(args)
         else:
             ach = bytes_cv / (cv_ms * 1e-3) / 1e9
             kname = ("cv_wta_row_kernel + cv_wta_fixup_kernel (certified fused cost volume + WTA)"

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -65,6 +66,54 @@ def _compile(src: str, force: bool) -> str:
     return obj
 
 
+_EXIT_CALL = re.compile(r"\b(call|jmp)\s+[0-9a-f]+\s+<(atexit|__cxa_atexit|on_exit)(@plt)?>")
+_FUNC_HDR = re.compile(r"^[0-9a-f]+ <(.+)>:$")
+
+
+def exit_hooks(lib: str):
+    """Exit-time code registered by `lib` (a rocprofv3 run of a cooperative-launch variant
+    crashed inside exit(), in a handler that reached the HIP runtime after the profiler had finalised).
+    Returns [(function, instruction)] for every call of atexit / __cxa_atexit / on_exit outside a hipcc
+    module constructor (__hip_module_ctor registers __hip_module_dtor, which unregisters the fat binary:
+    the one exit-time HIP call every hipcc object carries), plus the .fini_array entries other than the
+    C runtime's __do_fini.  Empty = no C++ static destructor, function-local static with a destructor or
+    explicit atexit handler of ours runs at exit."""
+    objdump = shutil.which("objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    r = subprocess.run([objdump, "-d", "--no-show-raw-insn", lib], capture_output=True, text=True, check=True)
+    bad, func = [], "?"
+    for line in r.stdout.splitlines():
+        m = _FUNC_HDR.match(line.strip())
+        if m:
+            func = m.group(1)
+            continue
+        if _EXIT_CALL.search(line) and func not in ("__hip_module_ctor", "atexit", "__cxa_atexit@plt"):
+            bad.append((func, line.strip()))
+    nm = subprocess.run(["nm", lib], capture_output=True, text=True, check=True).stdout
+    addr = {}
+    for ln in nm.splitlines():
+        parts = ln.split()
+        if len(parts) == 3:
+            addr.setdefault(int(parts[0], 16), parts[2])
+    # .fini_array entries are R_X86_64_RELATIVE relocations into the section: their addends are the targets
+    sec = subprocess.run(["readelf", "-S", "-W", lib], capture_output=True, text=True, check=True).stdout
+    lo = hi = 0
+    for ln in sec.splitlines():
+        if ".fini_array" in ln:
+            t = ln.split("]", 1)[1].split()
+            lo = int(t[2], 16)
+            hi = lo + int(t[4], 16)
+    rel = subprocess.run(["readelf", "-r", "-W", lib], capture_output=True, text=True, check=True).stdout
+    for ln in rel.splitlines():
+        t = ln.split()
+        if len(t) >= 4 and t[2] == "R_X86_64_RELATIVE":
+            off = int(t[0], 16)
+            if lo <= off < hi:
+                name = addr.get(int(t[3], 16), t[3])
+                if name not in ("__do_fini", "__do_global_dtors_aux"):
+                    bad.append((".fini_array", name))
+    return bad
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     srcs = sources()
@@ -80,6 +129,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        hooks = exit_hooks(tmp)
+        if hooks:
+            raise RuntimeError("libsde.so would run code of its own inside exit() (after the HIP runtime or a "
+                               "profiler may have finalised): " + "; ".join(f"{f}: {i}" for f, i in hooks[:10]))
         os.replace(tmp, LIB)
     if verbose:
         print(f"built {LIB}", file=sys.stderr)

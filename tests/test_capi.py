@@ -228,3 +228,27 @@ def test_isa_lint_passes_on_the_built_library():
     if not objs or not os.path.exists(_isa_lint.LLVM):
         pytest.skip("no built objects / ROCm LLVM tools")
     assert _isa_lint.lint_objects(objs) == []
+
+
+def test_library_registers_no_exit_time_code(tmp_path):
+    """code of ours inside exit() can reach the HIP runtime after it (or a profiler) has
+    finalised -- the build refuses it.  The built library carries only the hipcc module destructors; a C++
+    static with a destructor and a destructor-attribute function are both flagged."""
+    import shutil
+    import subprocess
+
+    from scenedepthestimation_amd import _build
+    if not os.path.exists(_build.LIB):
+        pytest.skip("libsde.so not built")
+    if not shutil.which("g++") or not shutil.which("readelf"):
+        pytest.skip("no g++ / binutils")
+    assert _build.exit_hooks(_build.LIB) == []
+    src = tmp_path / "hooks.cpp"
+    src.write_text("volatile int g;\nstruct S { ~S(); }; S::~S() {} static S s;\n"
+                   "__attribute__((destructor)) static void bye() { g = 1; }\n"
+                   "extern \"C\" int f() { static S t; return 1; }\n")
+    so = tmp_path / "libhooks.so"
+    subprocess.run(["g++", "-shared", "-fPIC", "-O1", str(src), "-o", str(so)], check=True)
+    hooks = _build.exit_hooks(str(so))
+    assert any(f == ".fini_array" for f, _ in hooks), hooks
+    assert sum(1 for f, _ in hooks if f != ".fini_array") >= 2, hooks   # the static and the local static

@@ -83,6 +83,21 @@ static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
 #define H16_ACT_AUX 1
 #endif
 
+// Probe 16384: per-phase s_memtime sums, written by lane 0 of every wave as 4 floats to out[32 blockIdx.x + 4 wave ..]
+// at the end (MFMA waves: c-block MFMAs, epilogue, barrier wait; stagers: work, barrier wait).
+__device__ float *h16_probe_out;   // set by the kernel before the stagers start (probe 16384)
+__device__ __forceinline__ uint64_t h16_stamp()
+{
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the stamp is back before any counted LDS wait
+    return t;
+}
+__device__ __forceinline__ void h16_stamp_out(float *out, int wave, int lane, const uint64_t (&ph)[4])
+{
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) out[32 * blockIdx.x + 4 * wave + k] = (float)ph[k];
+}
+
 // Split 4 channels, scaled by s, into the stage's (part, quarter) planes at dst (the unit's byte offset
 // in the stage, see h16_stager_loop).
 __device__ __forceinline__ void h16_put(char *dst, float4 v, float s)
@@ -189,14 +204,23 @@ __device__ __forceinline__ void h16_stager_loop(char *hsm, const float *__restri
     __syncthreads();
     // step i: the MFMA waves consume stage i & 1; here step i+1's halves are stored and step
     // i+2's loaded
+    uint64_t ph[4] = {0, 0, 0, 0};
 #pragma unroll 1
     for (int i = 0; i < nsteps; i++) {
+        const uint64_t t0 = (H16_DIAG & 16384) ? h16_stamp() : 0;
         if (2 * i + 2 < nh) store(ra, 2 * i + 2);
         if (2 * i + 4 < nh) load(ra, 2 * i + 4);
         if (2 * i + 3 < nh) store(rb, 2 * i + 3);
         if (2 * i + 5 < nh) load(rb, 2 * i + 5);
+        const uint64_t t1 = (H16_DIAG & 16384) ? h16_stamp() : 0;
         __syncthreads();
+        if (H16_DIAG & 16384) {
+            const uint64_t t2 = h16_stamp();
+            ph[0] += t1 - t0;
+            ph[1] += t2 - t1;
+        }
     }
+    if (H16_DIAG & 16384) h16_stamp_out(h16_probe_out, (st >> 6) + 4, st & 63, ph);
 }
 
 // Stager waves, layer 2 (FIRST): the stage is conv1 (Cin = 1, 3x3, bias, ReLU; mc_cnn_brunch.py:31-48) of
@@ -391,10 +415,34 @@ __device__ __forceinline__ H16A h16_afrag(__amdgpu_buffer_rsrc_t ra, uint32_t vo
             // tap: the CU's L2 A traffic scaled by H16_AREAL / 4 at the same instruction count
             const bool real = !(H16_DIAG & 1024) || (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < H16_AREAL;
             const int kc = (p * 64 + 16 * qq) * 16;
-            const int k = (H16_DIAG & 256) ? kc : real ? ((((hf * XP_NCB * 9 + tap) * 2 + p) * 64 + 16 * qq) * 16) : kc;
+            // 2048: the tap-0 block's 8 chunks, permuted by the tap (A data changes every tap, every load an L1 hit)
+            const int hp = hf ^ (tap & 1), pp2 = p ^ ((tap >> 1) & 1), qp = qq ^ ((tap >> 2) & 1);
+            const int kperm = ((hp * XP_NCB * 9 * 2 + pp2) * 64 + 16 * qp) * 16;
+            const int k = (H16_DIAG & 2048) ? kperm : (H16_DIAG & 256) ? kc : real ? ((((hf * XP_NCB * 9 + tap) * 2 + p) * 64 + 16 * qq) * 16) : kc;
             a.f[p][qq] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, voff, cbo + k, 0));
         }
     return a;
+}
+
+// Probe H16_PF = d > 0: MFMA wave 0 touches every 128-B line of tap u = s + d's A fragments (both M-tiles, both
+// 16-channel blocks, both parts: 8 chunks of 1 KB = 64 lines, one lane per line) while tap s runs, so the four
+// waves' own loads of that tap (issued one tap ahead of use) hit the CU's L1 instead of each missing to L2.
+#ifndef H16_PF
+#define H16_PF 0
+#endif
+#ifndef H16_PF_ROT
+#define H16_PF_ROT 0
+#endif
+__device__ uint32_t pf_sink_g;
+__device__ __forceinline__ uint32_t h16_pf_lane(int lane)
+{
+    const int c = lane >> 3;
+    return (uint32_t)((c >> 2) * (XP_NCB * 9 * 2 * 64 * 16) + ((c >> 1) & 1) * (9 * 2 * 64 * 16) + (c & 1) * 1024 +
+                      (lane & 7) * 128);
+}
+__device__ __forceinline__ uint32_t h16_prefetch(__amdgpu_buffer_rsrc_t ra, uint32_t poff, int cbo, int tap)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(ra, poff, cbo + tap * 2048, 0);
 }
 
 struct H16B {
@@ -472,22 +520,37 @@ __device__ __forceinline__ H16B h16_bfrag12(const char *sb, int b)
 
 template <int PH>
 __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4], __amdgpu_buffer_rsrc_t ra,
-                                             uint32_t avoff, int cb, int ncb, const char *sb)
+                                             uint32_t avoff, int cb, int ncb, const char *sb, bool pfw,
+                                             uint32_t poff, uint32_t &pf_sink, uint32_t &pf_prev)
 {
     constexpr int NT = 9, NB = NT * 8;
     H16B ring[2];
     ring[0] = h16_bfrag12(sb, 0);
+    const H16A fa = abuf[PH % 4];
 #pragma unroll
     for (int s = 0; s < NT; s++) {
+        if (H16_PF > 0 && (H16_PF_ROT ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == (s & 3) : pfw)) {
+            const int u = s + H16_PF;
+            const uint32_t t = u < NT ? h16_prefetch(ra, poff, cb * H16_A_CB, u) : h16_prefetch(ra, poff, ncb * H16_A_CB, u - NT);
+            pf_sink ^= pf_prev;   // the previous prefetch's value, one tap later (no wait on this one)
+            pf_prev = t;
+        }
 #pragma unroll
         for (int hf = 0; hf < 2; hf++) {
             const int h = 2 * (s + 1) + hf;
             if (H16_DIAG & 64) {   // timing probe: the loads issued into slots 1-3, the MFMAs on slot 0 only
                 abuf[1 + (2 * s + hf) % 3] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
                                                         : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
-            } else if (!(H16_DIAG & 4))
+            } else if (!(H16_DIAG & (4 | 8192)))
                 abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
                                                 : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+        }
+        if (H16_DIAG & 4096) {   // probe: wait for this tap's ring slots as the product does, MFMAs on fa
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                const H16A &w = abuf[(2 * s + hf + PH) % 4];
+                asm volatile("" ::"v"(w.f[0][0]), "v"(w.f[0][1]), "v"(w.f[1][0]), "v"(w.f[1][1]));
+            }
         }
 #pragma unroll
         for (int rp = 0; rp < 8; rp++) {
@@ -510,7 +573,7 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
             } else {
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                const H16A &a = abuf[(H16_DIAG & (4 | 64)) ? 0 : (2 * s + hf + PH) % 4];
+                const H16A &a = (H16_DIAG & 4096) ? fa : abuf[(H16_DIAG & (4 | 64)) ? 0 : (2 * s + hf + PH) % 4];
 #pragma unroll
                 for (int qq = 0; qq < 2; qq++) {
                     floatx4 &c = acc[H16_AR(rp) * 4 + 2 * hf + qq];
@@ -763,6 +826,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     int tile = blockIdx.x;
     if (tile >= bt.ntiles) return;
     const float *hdr = wkblob + LK_F16 + LK_W;
+    if (H16_DIAG & 16384) h16_probe_out = out;   // every thread stores the same value
     if (wave >= 4) {
         if (FIRST) h16_conv1_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr, w1blob);
         else if (ISPL) h16_dma_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS);
@@ -777,6 +841,9 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     const __amdgpu_buffer_rsrc_t ra = xp_rsrc(wkblob + LK_F16);
     // the lane's A-fragment byte offset: cb16 = 2 cb + (lane >> 5), channel half (lane >> 4) & 1, n & 15
     const uint32_t avoff = (uint32_t)((lane >> 5) * (9 * 2 * 64) + ((lane >> 4) & 1) * 32 + (lane & 15)) * 16u;
+    const uint32_t poff = h16_pf_lane(lane);
+    uint32_t pf_sink = 0u, pf_prev = 0u;
+    uint64_t pht[4] = {0, 0, 0, 0};
     // the lane's B base: plane quarter lane >> 4, pixel (4g, lane & 15) of the input tile
     const int bbase = (lane >> 4) * H16_PLANE + ((4 * g) * XP_IX + (lane & 15)) * 16;
     // c-blocks feeding each B fragment to all four quarters (h16_cblock12), except the last layer with
@@ -787,6 +854,10 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
     if constexpr (RING) {
+        abuf[2] = h16_afrag(ra, avoff, 0, 2);
+        abuf[3] = h16_afrag(ra, avoff, 0, 3);
+    }
+    if (H16_DIAG & 8192) {   // probe: four distinct half-taps in the ring, never reloaded
         abuf[2] = h16_afrag(ra, avoff, 0, 2);
         abuf[3] = h16_afrag(ra, avoff, 0, 3);
     }
@@ -810,14 +881,16 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         for (int i = 0; i < 32; i++) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
         // cb 0, then cb 1 and the epilogue (as a lambda: B12 unrolls the pair, the 3-slot form keeps a loop)
         auto cstep = [&](int cb) {
+            const uint64_t ta = (H16_DIAG & 16384) ? h16_stamp() : 0;
             if constexpr (RING) {
                 h16_cblock12r<3>(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             } else if constexpr (B12) {
-                if (cb == 0) h16_cblock12<0>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
-                else h16_cblock12<2>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
+                if (cb == 0) h16_cblock12<0>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase, g == 0, poff, pf_sink, pf_prev);
+                else h16_cblock12<2>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase, g == 0, poff, pf_sink, pf_prev);
             } else {
                 h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             }
+            const uint64_t tb = (H16_DIAG & 16384) ? h16_stamp() : 0;
             if (cb == H16_NCB - 1) {
                 if (img != sc_img) {
                     const float *am = in_amax + img * bt.amax_stride;
@@ -833,7 +906,14 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
                 h16_epilogue<LAST, OUT_CB, SPLIT, OSPL>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi,
                                                        olo, onrm, amax_run, amax_img, out_amax, sc_o);
             }
+            const uint64_t tc = (H16_DIAG & 16384) ? h16_stamp() : 0;
             __syncthreads();
+            if (H16_DIAG & 16384) {
+                const uint64_t td = h16_stamp();
+                pht[0] += tb - ta;
+                pht[1] += tc - tb;
+                pht[2] += td - tc;
+            }
             cur ^= 1;
         };
         if constexpr (B12) {
@@ -845,6 +925,8 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         }
     }
     if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, bt.amax_stride);
+    if (H16_PF > 0 && (pf_sink ^ pf_prev) == 0x12345679u) pf_sink_g = 1u;   // keeps the prefetches (never true in practice)
+    if (H16_DIAG & 16384) h16_stamp_out(out, g, lane, pht);   // tile-0 rows: written in round 0, long done
     if ((H16_DIAG & 8) && wave == 0 && lane == 0) {
         const uint64_t c = __builtin_amdgcn_s_memtime() - clk0, r = __builtin_amdgcn_s_memrealtime() - rt0;
         out[2 * blockIdx.x] = (float)c;
