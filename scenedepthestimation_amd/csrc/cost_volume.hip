@@ -597,6 +597,28 @@ __global__ __launch_bounds__(256) void argmin_merge_kernel(const float *__restri
     disp[p] = (float)arg;
 }
 
+// Chunked certified CV + WTA (sde_cv_wta, D past one row sweep's LDS window): chunk k's exact first-minimum
+// (value, index) per pixel at mins / args + k * npix, chunks ordered by d; the pixel's first minimum over
+// all of them (strict <: a later chunk wins only with a smaller cost -- a sequential scan over d), written
+// to whichever outputs are requested.
+__global__ __launch_bounds__(256) void argmin_chunks_kernel(const float *__restrict__ mins,
+                                                            const int32_t *__restrict__ args, int nchunks,
+                                                            int64_t npix, float *__restrict__ disp,
+                                                            float *__restrict__ out_min, int32_t *__restrict__ out_arg)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    float best = mins[p];
+    int arg = args[p];
+    for (int k = 1; k < nchunks; k++) {
+        const float m = mins[(size_t)k * npix + p];
+        if (m < best) { best = m; arg = args[(size_t)k * npix + p]; }
+    }
+    if (disp) disp[p] = (float)arg;
+    if (out_min) out_min[p] = best;
+    if (out_arg) out_arg[p] = arg;
+}
+
 // ===========================================================================
 // Certified fast path for the fused cost volume + WTA (north-star kernel).
 //
@@ -953,6 +975,17 @@ SDE_EXPORT int64_t sde_cv_wta_workspace_bytes(int H, int W)
     return cert_ws_bytes(H, W, true);
 }
 
+// chunked row sweep: [counter, list] then the chunks' (min, arg) planes; INT64_MAX when [d0, d1) does not split
+// into row-sweep-supported chunks (the chunk kernel path then runs)
+constexpr int ROW_CHUNK = 256;
+static int64_t row_chunk_layout(int H, int W, int d0, int d1)
+{
+    const int K = cdiv(d1 - d0, ROW_CHUNK);
+    for (int k = 0; k < K; k++)
+        if (!row_cert_supported(d0 + k * ROW_CHUNK, std::min(d1, d0 + (k + 1) * ROW_CHUNK))) return INT64_MAX;
+    return cert_ws_bytes(H, W, false) + (int64_t)K * 8 * H * W;
+}
+
 SDE_EXPORT int sde_feature_split(const float *feat, int64_t npix, int C, uint16_t *hi, uint16_t *lo, float *norm,
                                  void *stream)
 {
@@ -1012,6 +1045,26 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
         if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
         launch_row_cert(fl, fr, H, W, d0, d1, min_cost, argmin, disp, counter, list, st);
         cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
+    } else if (C == 64 && mode == SDE_CV_CERTIFIED && row_chunk_layout(H, W, d0, d1) <= sde_cv_wta_workspace_bytes(H, W)) {
+        // D past the row sweep's LDS window (e.g. BASELINE config 5, D = 512): ROW_CHUNK-disparity chunks, each
+        // through the row-sweep kernel + its exact fix-ups (the same outputs as the exact kernel on that
+        // range, as for the disparity shards of parallel.py), then the first minimum over the chunks in d order
+        if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
+        const int64_t npix = (int64_t)H * W;
+        const int K = cdiv(d1 - d0, ROW_CHUNK);
+        unsigned *counter = reinterpret_cast<unsigned *>(workspace);
+        int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
+        float *cmin = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + cert_ws_bytes(H, W, false));
+        int32_t *carg = reinterpret_cast<int32_t *>(cmin + (size_t)K * npix);
+        for (int k = 0; k < K; k++) {
+            const int a = d0 + k * ROW_CHUNK, b = std::min(d1, a + ROW_CHUNK);
+            if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+            launch_row_cert(fl, fr, H, W, a, b, cmin + (size_t)k * npix, carg + (size_t)k * npix, nullptr, counter,
+                            list, st);
+            cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, a, b, counter, list, cmin + (size_t)k * npix,
+                                                      carg + (size_t)k * npix, nullptr);
+        }
+        argmin_chunks_kernel<<<cdiv(npix, 256), 256, 0, st>>>(cmin, carg, K, npix, disp, min_cost, argmin);
     } else if (C == 64 && mode == SDE_CV_CERTIFIED) {
         if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
         const int64_t npix = (int64_t)H * W;

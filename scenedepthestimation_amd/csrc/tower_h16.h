@@ -60,19 +60,15 @@ static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
 #endif
 
 // Split 4 channels, scaled by s, into the stage's (part, quarter) planes at dst (the unit's byte offset
-// in the stage, see h16_stager_loop).
+// in the stage, see h16_stager_loop): hi = f16(x s) by packed converts, lo = f16(x s - hi) by v_fma_mix from the
+// packed hi half (xp_split16s; x s - hi is exact in fp32, so the same bits as the per-value split).  8 instead of
+// 20 VALU per unit: the stagers' work per launch 222 -> 136 kcycles (profiles/r06/tower_phase_*.txt).
 __device__ __forceinline__ void h16_put(char *dst, float4 v, float s)
 {
-    f16x4 p0, p1;
-    const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        const _Float16 hh = (_Float16)xs[e];
-        p0[e] = hh;
-        p1[e] = (_Float16)(xs[e] - (float)hh);
-    }
-    *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, p0);
-    *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, p1);
+    u32x2 hw, lw;
+    xp_split16s(make_float4(v.x * s, v.y * s, v.z * s, v.w * s), hw, lw);
+    *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, hw);
+    *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, lw);
 }
 
 // Stage unit (pixel << 2 | 4-channel chunk) of stager thread st at iteration i: a wave's lanes take 16
@@ -424,13 +420,19 @@ __device__ __forceinline__ H16B h16_bfrag12(const char *sb, int b)
     return f;
 }
 
-template <int PH>
+// BRD: depth of the B ring (fragments read BRD - 1 (row, half) steps ahead).  Depth 3 (two steps, 24 MFMAs
+// ahead) takes the MFMA waves' c-block loop from 280 to 249-274 kcycles per launch against the 232-kcycle MFMA floor
+// (phase stamps, profiles/r06/tower_phase_*.txt): the LDS latency of a one-step-ahead read was showing.  The 8
+// more VGPRs fit the middle layers' c-block-layout instantiation without spills; the others keep depth 2.
+template <int PH, int BRD>
 __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4], __amdgpu_buffer_rsrc_t ra,
                                              uint32_t avoff, int cb, int ncb, const char *sb)
 {
     constexpr int NT = 9, NB = NT * 8;
-    H16B ring[2];
-    ring[0] = h16_bfrag12(sb, 0);
+    static_assert(NB % BRD == 0, "static B ring slots");
+    H16B ring[BRD];
+#pragma unroll
+    for (int k = 0; k < BRD - 1; k++) ring[k] = h16_bfrag12(sb, k);
 #pragma unroll
     for (int s = 0; s < NT; s++) {
 #pragma unroll
@@ -443,8 +445,8 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
         for (int rp = 0; rp < 8; rp++) {
             const int b = s * 8 + rp;
             __builtin_amdgcn_sched_barrier(0);
-            const H16B &bf = ring[b & 1];
-            if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
+            const H16B &bf = ring[b % BRD];
+            if (b + BRD - 1 < NB) ring[(b + BRD - 1) % BRD] = h16_bfrag12(sb, b + BRD - 1);
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
                 const H16A &a = abuf[(2 * s + hf + PH) % 4];
@@ -671,6 +673,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     // c-blocks feeding each B fragment to all four quarters (h16_cblock12), except the last layer with
     // split outputs (its epilogue would spill 13 VGPRs with the 2-tap A ring)
     constexpr bool B12 = H16_B12 == 2 ? !(LAST && SPLIT) : H16_B12 == 1 ? !LAST && !FIRST : false;
+    constexpr int BRD = (IN_CB && OUT_CB && !FIRST && !LAST && !ISPL && !OSPL) ? 3 : 2;
     H16A abuf[4];   // h16_cblock: slots 0-2
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
@@ -690,8 +693,8 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         // cb 0, then cb 1 and the epilogue (as a lambda: B12 unrolls the pair, the 3-slot form keeps a loop)
         auto cstep = [&](int cb) {
             if constexpr (B12) {
-                if (cb == 0) h16_cblock12<0>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
-                else h16_cblock12<2>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
+                if (cb == 0) h16_cblock12<0, BRD>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
+                else h16_cblock12<2, BRD>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
             } else {
                 h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             }

@@ -774,7 +774,9 @@ def test_certified_golden(gpu, golden, golden_cases):
 @pytest.mark.parametrize("H,W,D,d0", [(3, 200, 64, 0), (2, 333, 192, 0), (2, 130, 256, 0), (2, 700, 512, 0),
                                       (3, 97, 100, 0), (2, 300, 192, 40), (2, 64, 192, 0), (1, 5, 9, 0),
                                       (2, 1000, 192, 0), (2, 129, 100, 33), (3, 250, 256, 17), (2, 70, 1, 0),
-                                      (2, 600, 288, 32)])
+                                      (2, 600, 288, 32),
+                                      # past one row sweep's window: 256-disparity chunks merged in d order
+                                      (2, 900, 700, 5), (3, 300, 600, 100)])
 def test_certified_matches_exact(gpu, oracle, H, W, D, d0):
     rng = np.random.default_rng(H * 1000 + W + D)
     fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
@@ -786,13 +788,18 @@ def test_certified_matches_exact(gpu, oracle, H, W, D, d0):
     assert np.array_equal(o["certified"][2], oam) and o["certified"][1].tobytes() == omn.tobytes()
 
 
-def test_certified_adversarial_ties_and_nonfinite(gpu, oracle):
+@pytest.mark.parametrize("W,D", [(260, 96), (700, 512)])
+def test_certified_adversarial_ties_and_nonfinite(gpu, oracle, W, D):
+    """D = 512: the chunked row sweep, with exact ties straddling the 256-disparity chunk boundary."""
     rng = np.random.default_rng(123)
-    H, W, D = 4, 260, 96
+    H = 4
     fl = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
     fr = l2n(rng.standard_normal((H, W, 64)).astype(np.float32))
     fr[0] = fr[0, 7]                       # a constant row: every valid d ties exactly
     fr[1, 100:160] = fr[1, 40:100]         # periodic texture: exact ties at two disparities
+    if D > 256:
+        fl[1, 600] = fr[1, 600 - 200]      # the same best at d = 200 and d = 300 (either side of the boundary)
+        fr[1, 300] = fr[1, 400]
     fr[2, :, :32] *= 1.0 + 1e-6            # near-ties below the fast path's resolution
     fl[3, 50] = np.inf                     # non-finite features take the exact path
     fr[3, 10] = np.nan

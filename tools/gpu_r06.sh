@@ -12,7 +12,7 @@ tail -1 $O/smoke.log
 fi
 timeout -k 10 400 python bench.py > $O/bench_north_star.json 2> $O/bench_north_star.err || { tail -20 $O/bench_north_star.err; exit 1; }
 tail -c 400 $O/bench_north_star.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_north_star -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_bench_north_star.json 2> $O/prof_north_star.err || { tail -20 $O/prof_north_star.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_north_star -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-c3 > $O/prof_bench_north_star.json 2> $O/prof_north_star.err || { tail -20 $O/prof_north_star.err; exit 1; }
 if ls tools/_var/libsde_*.so > /dev/null 2>&1; then
   timeout -k 10 300 python tools/tower_variants.py 1024 > $O/tower_variants.txt 2>&1 || { tail -20 $O/tower_variants.txt; exit 1; }
   grep -E "us |clock" $O/tower_variants.txt | tail -24

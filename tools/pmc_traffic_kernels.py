@@ -17,7 +17,7 @@ import subprocess
 import sys
 
 KERNELS = {   # key -> (substring of the kernel name, sum over distinct names) or [(substring, dispatches per unit)]
-    "tower_conv64_layer": ("conv64_x6p_kernel<false, false, true, true, true>", False),
+    "tower_conv64_layer": ("conv64_h16_kernel<false, true, true, false, false, false, false>", False),
     "cv_wta_row": ("cv_wta_row2_kernel<false>", False),
     "cvlr": ("cvlr3_kernel", False),
     # one sde_cbca_lr call at 2 iterations: 2 transposes, 2 x (horizontal + vertical pass), 1 shear

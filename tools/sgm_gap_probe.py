@@ -1,6 +1,6 @@
 """Probe of the SGM pair's process-to-process spread ("LR/RL 0.80 vs 0.95 ms"): the
 7-launch sde_sgm_8path_wta_pair at 1024^2 x 192 timed with HIP events in THIS process for the in-tree
-library and the tools/_var/libsde_sgmgap*.so probe builds (SRC=tools/variants/sgm_gap.hip bash
+library and the tools/_var/libsde_sgmgap*.so probe builds (SRC=tools/variants/sgm_probe.hip bash
 tools/build_file_variant.sh sgm.hip sgmgapN -DSGM_GAP=N; SGM_GAP: 1 = host sync between passes,
 2 = an event record with a system-scope release between passes, 3 = a plain event record), round-robin,
 median of 7.  The per-launch split comes from a rocprofv3 --kernel-trace run of this same script."""

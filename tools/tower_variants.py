@@ -30,7 +30,7 @@ nws = ops.tower_batch_workspace_bytes(H, W, 2, L)
 ws = torch.empty(nws, dtype=torch.uint8, device="cuda")
 P, I = ctypes.c_void_p, ctypes.c_int
 here = os.path.dirname(os.path.abspath(__file__))
-sos = [_lib.LIB] + sorted(glob.glob(os.path.join(here, "_var", "libsde_*.so")))
+sos = [_lib.LIB] + sorted(glob.glob(os.path.join(here, "_var", os.environ.get("SDE_VAR_GLOB", "libsde_*.so"))))
 libs = []
 for so in sos:
     lib = ctypes.CDLL(so)

@@ -1,6 +1,8 @@
-// sgm_gap.hip -- PROBE COPY of scenedepthestimation_amd/csrc/sgm.hip with the SGM_GAP switch (what sits between
-// two passes of the pair; tools/sgm_gap_probe.py).  Build: SRC=tools/variants/sgm_gap.hip bash
-// tools/build_file_variant.sh sgm.hip sgmgapN -DSGM_GAP=N.  Never part of libsde.so.
+// sgm_probe.hip -- PROBE COPY of scenedepthestimation_amd/csrc/sgm.hip with timing switches.  Never part of libsde.so.
+// SGM_GAP = N: what sits between two passes of the pair (tools/sgm_gap_probe.py).
+// SGM_SKEW = n > 0: line l's wave sleeps (l % SGM_SKEW_K) x n x 64 cycles before its first step, so the
+// 2048 concurrent line streams of a pass do not walk their rows in lock step (tools/sgm_skew_probe.py).
+// Build: SRC=tools/variants/sgm_probe.hip bash tools/build_file_variant.sh sgm.hip NAME -DSGM_GAP=N / -DSGM_SKEW=n.
 // sgm.hip -- semi-global matching and the GPU path's post-processing (gfx950).
 //
 // Replaces (process_functional.py):
@@ -42,6 +44,12 @@
 #define SGM_WTA_PARK 1
 #endif
 
+#ifndef SGM_SKEW
+#define SGM_SKEW 0
+#endif
+#ifndef SGM_SKEW_K
+#define SGM_SKEW_K 8
+#endif
 namespace sde {
 
 // direction table in the reference launch order: step (dr, dc) and P1 channel
@@ -558,6 +566,9 @@ __global__ __launch_bounds__(64) void sgm_scan_kernel(SgmSide s0, SgmSide s1, in
     g.n = nlen - 1 > 2 ? nlen - 1 : 2;
     const int line = blockIdx.x;
     const int lane = threadIdx.x & 63;      // one wave per block: lane < 64 known to the compiler
+#if SGM_SKEW > 0
+    for (int k = line % SGM_SKEW_K; k > 0; k--) __builtin_amdgcn_s_sleep(SGM_SKEW);
+#endif
     const int dbase = lane * DPL;
     const double INF = __builtin_inf();
     // fused WTA: per-step lane partials of the last PF steps (wave-private: one wave per block).

@@ -72,6 +72,9 @@ static_assert(H16_SMEM_FIRST <= 163840, "LDS (layer 2)");
 #ifndef H16_RING
 #define H16_RING 2
 #endif
+#ifndef H16_BRD
+#define H16_BRD 2   // probe: B ring depth of the B12 c-block (fragments read H16_BRD - 1 steps ahead)
+#endif
 #ifndef H16_AREAL
 #define H16_AREAL 1
 #endif
@@ -100,8 +103,21 @@ __device__ __forceinline__ void h16_stamp_out(float *out, int wave, int lane, co
 
 // Split 4 channels, scaled by s, into the stage's (part, quarter) planes at dst (the unit's byte offset
 // in the stage, see h16_stager_loop).
+#ifndef H16_FASTPUT
+#define H16_FASTPUT 0   // probe: the split by a packed hi convert + v_fma_mix lo (xp_split16s; the same bits)
+#endif
+#ifndef H16_SPRIO
+#define H16_SPRIO 0     // probe: s_setprio of the stager waves
+#endif
 __device__ __forceinline__ void h16_put(char *dst, float4 v, float s)
 {
+    if (H16_FASTPUT) {
+        u32x2 hw, lw;
+        xp_split16s(make_float4(v.x * s, v.y * s, v.z * s, v.w * s), hw, lw);
+        *reinterpret_cast<uint2 *>(dst) = __builtin_bit_cast(uint2, hw);
+        *reinterpret_cast<uint2 *>(dst + 4 * H16_PLANE) = __builtin_bit_cast(uint2, lw);
+        return;
+    }
     f16x4 p0, p1;
     const float xs[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
 #pragma unroll
@@ -524,8 +540,9 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
                                              uint32_t poff, uint32_t &pf_sink, uint32_t &pf_prev)
 {
     constexpr int NT = 9, NB = NT * 8;
-    H16B ring[2];
-    ring[0] = h16_bfrag12(sb, 0);
+    H16B ring[H16_BRD];
+#pragma unroll
+    for (int k = 0; k < H16_BRD - 1; k++) ring[k] = h16_bfrag12(sb, k);
     const H16A fa = abuf[PH % 4];
 #pragma unroll
     for (int s = 0; s < NT; s++) {
@@ -556,8 +573,8 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
         for (int rp = 0; rp < 8; rp++) {
             const int b = s * 8 + rp;
             __builtin_amdgcn_sched_barrier(0);
-            const H16B &bf = ring[b & 1];
-            if (b + 1 < NB) ring[(b + 1) & 1] = h16_bfrag12(sb, b + 1);
+            const H16B &bf = ring[b % H16_BRD];
+            if (b + H16_BRD - 1 < NB) ring[(b + H16_BRD - 1) % H16_BRD] = h16_bfrag12(sb, b + H16_BRD - 1);
             if (H16_ORDER == 1) {   // probe: B-major order (each accumulator's three products in the same order)
 #pragma unroll
                 for (int pp = 0; pp < 3; pp++)
@@ -828,6 +845,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     const float *hdr = wkblob + LK_F16 + LK_W;
     if (H16_DIAG & 16384) h16_probe_out = out;   // every thread stores the same value
     if (wave >= 4) {
+        if (H16_SPRIO) __builtin_amdgcn_s_setprio(H16_SPRIO);
         if (FIRST) h16_conv1_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr, w1blob);
         else if (ISPL) h16_dma_stager_loop(hsm, in, Hin, Win, bt, tid - XP_STAGERS);
         else h16_stager_loop<IN_CB>(hsm, in, Hin, Win, bt, tid - XP_STAGERS, in_amax, hdr);
