@@ -960,7 +960,9 @@ SDE_EXPORT int sde_cost_volume(const float *fl, const float *fr, int H, int W, i
     return launch_status();
 }
 
-// certified-mode workspace: [counter 256 B][list 4*npix][planes 4 x 128*npix][norms 2 x 4*npix]
+// certified-mode workspace: [counters 256 B][list 4*npix][planes 4 x 128*npix][norms 2 x 4*npix]; the fix-up
+// count of a call is the sum of the 64 counter words (one per disparity chunk, sde_cv_wta's chunked path)
+constexpr int CERT_COUNTERS = 64;
 static int64_t cert_ws_bytes(int H, int W, bool with_planes)
 {
     const int64_t npix = (int64_t)H * W;
@@ -981,6 +983,7 @@ constexpr int ROW_CHUNK = 256;
 static int64_t row_chunk_layout(int H, int W, int d0, int d1)
 {
     const int K = cdiv(d1 - d0, ROW_CHUNK);
+    if (K > CERT_COUNTERS) return INT64_MAX;
     for (int k = 0; k < K; k++)
         if (!row_cert_supported(d0 + k * ROW_CHUNK, std::min(d1, d0 + (k + 1) * ROW_CHUNK))) return INT64_MAX;
     return cert_ws_bytes(H, W, false) + (int64_t)K * 8 * H * W;
@@ -1000,7 +1003,7 @@ static int launch_cert(const float *fl, const float *fr, const uint16_t *lhi, co
 {
     unsigned *counter = reinterpret_cast<unsigned *>(ws);
     int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(ws) + 256);
-    if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+    if (hipMemsetAsync(counter, 0, CERT_COUNTERS * sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
     cv_wta_cert_kernel<<<cdiv(W, FX_NX) * H, 256, 0, st>>>(
         fl, fr, reinterpret_cast<const uint4 *>(lhi), reinterpret_cast<const uint4 *>(llo), lnrm,
         reinterpret_cast<const uint4 *>(rhi), reinterpret_cast<const uint4 *>(rlo), rnrm, H, W, d0, d1, min_cost,
@@ -1042,7 +1045,7 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
         if (!workspace || workspace_bytes < sde_cv_wta_workspace_bytes(H, W)) return SDE_ERR_WORKSPACE;
         unsigned *counter = reinterpret_cast<unsigned *>(workspace);
         int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
-        if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
+        if (hipMemsetAsync(counter, 0, CERT_COUNTERS * sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
         launch_row_cert(fl, fr, H, W, d0, d1, min_cost, argmin, disp, counter, list, st);
         cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, d0, d1, counter, list, min_cost, argmin, disp);
     } else if (C == 64 && mode == SDE_CV_CERTIFIED && row_chunk_layout(H, W, d0, d1) <= sde_cv_wta_workspace_bytes(H, W)) {
@@ -1056,12 +1059,14 @@ SDE_EXPORT int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C,
         int32_t *list = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(workspace) + 256);
         float *cmin = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + cert_ws_bytes(H, W, false));
         int32_t *carg = reinterpret_cast<int32_t *>(cmin + (size_t)K * npix);
+        // chunk k counts its fix-ups in counter word k (sde_cv_wta_fixups-style readers sum the words); the
+        // list is reused: chunk k's fix-ups run before chunk k + 1's sweep
+        if (hipMemsetAsync(counter, 0, CERT_COUNTERS * sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
         for (int k = 0; k < K; k++) {
             const int a = d0 + k * ROW_CHUNK, b = std::min(d1, a + ROW_CHUNK);
-            if (hipMemsetAsync(counter, 0, sizeof(unsigned), st) != hipSuccess) return SDE_ERR_LAUNCH;
-            launch_row_cert(fl, fr, H, W, a, b, cmin + (size_t)k * npix, carg + (size_t)k * npix, nullptr, counter,
-                            list, st);
-            cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, a, b, counter, list, cmin + (size_t)k * npix,
+            launch_row_cert(fl, fr, H, W, a, b, cmin + (size_t)k * npix, carg + (size_t)k * npix, nullptr, counter + k,
+                            list, st, k > 0 ? cmin + (size_t)(k - 1) * npix : nullptr);
+            cv_wta_fixup_kernel<<<1024, 256, 0, st>>>(fl, fr, W, a, b, counter + k, list, cmin + (size_t)k * npix,
                                                       carg + (size_t)k * npix, nullptr);
         }
         argmin_chunks_kernel<<<cdiv(npix, 256), 256, 0, st>>>(cmin, carg, K, npix, disp, min_cost, argmin);

@@ -84,6 +84,6 @@ constexpr float FX_NORM_UP = 1.000004f;
 // the row-sweep kernel (cv_row.hip): window size limit and launcher
 bool row_cert_supported(int d0, int d1);
 void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int d1, float *out_min, int32_t *out_arg,
-                     float *out_disp, unsigned *counter, int32_t *list, hipStream_t st);
+                     float *out_disp, unsigned *counter, int32_t *list, hipStream_t st, const float *prev_min = nullptr);
 
 }  // namespace sde

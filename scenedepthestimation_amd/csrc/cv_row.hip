@@ -289,7 +289,11 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
             const size_t p = rowpix + x;
             // certified only when every operand is finite and no fp16 part can overflow (then
             // every score and eps are finite too)
-            if (!lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX && (best - second) > 2.0f * eps && arg >= 0) {
+            // x < d0: no voxel of the band is inside the image -- every cost is the -0.0 fill, so the scan's
+            // first minimum is d0 whatever the features hold (the chunked path's later chunks: x < 256 k)
+            const bool none = x < d0;
+            if (none || (!lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX && (best - second) > 2.0f * eps && arg >= 0)) {
+                if (none) arg = d0;
                 if (WANT_MIN) {
                     float cost = -0.0f;
                     if (x - arg >= 0)
@@ -378,12 +382,16 @@ __device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *
     }
 }
 
+// prev_min (chunked path, chunks after the first): the previous chunk's exact first-minimum cost per pixel.  A pixel
+// whose every exact score here is provably below -prev_min (best fast score + eps, with a factor 2 for the add's
+// rounding) has every cost above the previous chunk's minimum, so this chunk cannot win the in-order merge: it
+// writes (+inf, -1) and skips the certificate and the fix-up.
 template <bool WANT_MIN>
 __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
                                                           int H, int W, int d0, int d1, int tlo0, int nw, int nt,
                                                           float *__restrict__ out_min, int32_t *__restrict__ out_arg,
                                                           float *__restrict__ out_disp, unsigned *__restrict__ counter,
-                                                          int32_t *__restrict__ list)
+                                                          int32_t *__restrict__ list, const float *__restrict__ prev_min)
 {
     extern __shared__ __attribute__((aligned(16))) uint4 rsm2[];
     uint4 *ring = rsm2;                                             // [nt][2 planes][32 px][8 chunks]
@@ -660,7 +668,13 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
             const float nr = sqrtf(__uint_as_float(nmax2)) * FX_NORM_UP;
             const float eps = (RW_K * nl * nr + RW_ABS * (nl + nr) + FX_ABS) * (RW_SCALE * RW_SCALE);
             const size_t p = rowpix + x;
-            if (!lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX && (best - second) > 2.0f * eps && arg >= 0) {
+            const bool none = x < d0;   // as in cv_wta_row_kernel: every cost the -0.0 fill, first minimum d0
+            const bool fin = !lbad && !wbad && nl < RW_NMAX && nr < RW_NMAX;
+            if (!none && fin && WANT_MIN && prev_min && best + 2.0f * eps < -prev_min[p] * (RW_SCALE * RW_SCALE)) {
+                out_min[p] = __builtin_inff();
+                if (out_arg) out_arg[p] = -1;
+            } else if (none || (fin && (best - second) > 2.0f * eps && arg >= 0)) {
+                if (none) arg = d0;
                 if (WANT_MIN) {
                     float cost = -0.0f;
                     if (x - arg >= 0)
@@ -714,7 +728,7 @@ bool row_cert_supported(int d0, int d1)
 }
 
 void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int d1, float *out_min, int32_t *out_arg,
-                     float *out_disp, unsigned *counter, int32_t *list, hipStream_t st)
+                     float *out_disp, unsigned *counter, int32_t *list, hipStream_t st, const float *prev_min)
 {
     static std::atomic<uint64_t> attr{0};
     constexpr int NT2 = 512;
@@ -734,10 +748,12 @@ void launch_row_cert(const float *fl, const float *fr, int H, int W, int d0, int
         const int nt = nw + R2_NEW;
         if (out_min)
             cv_wta_row2_kernel<true><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
-                                                                          out_min, out_arg, out_disp, counter, list);
+                                                                          out_min, out_arg, out_disp, counter, list,
+                                                                          prev_min);
         else
             cv_wta_row2_kernel<false><<<H, NT2, row2_smem(nt), st>>>(fl, fr, H, W, d0, d1, tlo0, nw, nt,
-                                                                           nullptr, out_arg, out_disp, counter, list);
+                                                                           nullptr, out_arg, out_disp, counter, list,
+                                                                           nullptr);
         return;
     }
     int tlo0 = 0, ntw = 0;

@@ -424,7 +424,10 @@ __device__ __forceinline__ H16B h16_bfrag12(const char *sb, int b)
 // ahead) takes the MFMA waves' c-block loop from 280 to 249-274 kcycles per launch against the 232-kcycle MFMA floor
 // (phase stamps, profiles/r06/tower_phase_*.txt): the LDS latency of a one-step-ahead read was showing.  The 8
 // more VGPRs fit the middle layers' c-block-layout instantiation without spills; the others keep depth 2.
-template <int PH, int BRD>
+// NEXT = false (the c-block that ends a tile): the last tap does not request the next c-block's first tap; the
+// caller's epilogue does, once half the accumulators are stored (h16_epilogue's `mid`), so those 32 VGPRs are not
+// live across the whole epilogue -- what lets the 3-deep B ring fit layer 2 and the last layer without spills.
+template <int PH, int BRD, bool NEXT = true>
 __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4], __amdgpu_buffer_rsrc_t ra,
                                              uint32_t avoff, int cb, int ncb, const char *sb)
 {
@@ -438,8 +441,9 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
 #pragma unroll
         for (int hf = 0; hf < 2; hf++) {
             const int h = 2 * (s + 1) + hf;
-            abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
-                                            : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
+            if (NEXT || h < H16_HT)
+                abuf[(h + PH) % 4] = h < H16_HT ? h16_afrag(ra, avoff, cb * H16_A_CB, h)
+                                                : h16_afrag(ra, avoff, ncb * H16_A_CB, h - H16_HT);
         }
 #pragma unroll
         for (int rp = 0; rp < 8; rp++) {
@@ -470,13 +474,13 @@ __device__ __forceinline__ void h16_cblock12(floatx4 (&acc)[32], H16A (&abuf)[4]
 // Tile epilogue of one MFMA wave (rows 4g ..): unscale + bias, then ReLU + c-block-major stores
 // (+ the running bound word), or (LAST) the L2 norm and [h][w][64] stores.  Stored registers are
 // pinned live for XP_PIN stores, as in xp_epilogue ("store-data overwrite").
-template <bool LAST, bool OUT_CB, bool SPLIT, bool OSPL>
+template <bool LAST, bool OUT_CB, bool SPLIT, bool OSPL, typename MID>
 __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane, int g, int img, int ty0, int tx0,
                                              float unscale, const float4 *lbias4, float *__restrict__ out, int Hout,
                                              int Wout, const XpBatch &bt, uint16_t *__restrict__ ohi,
                                              uint16_t *__restrict__ olo, float *__restrict__ onrm,
                                              uint32_t &amax_run, int &amax_img, float *__restrict__ out_amax,
-                                             float oscale)
+                                             float oscale, MID &&mid)
 {
     static_assert(!OSPL || (!LAST && !OUT_CB), "split outputs: intermediate layers");
     int j = lane & 15, k4 = lane >> 4;
@@ -494,6 +498,10 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
         // store each, to plane part = k4 & 1
         const uint32_t pb = (uint32_t)HW * 16u;
         const uint32_t ospl_lane = (uint32_t)((k4 & 1) * 4 + (k4 >> 1)) * pb;
+        // FULL: every row and column of the tile is inside the output (all but the last tile row and column):
+        // no per-row branches, no per-lane range selects
+        auto body = [&](auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float4 b4 = lbias4[4 * q + k4];
@@ -505,12 +513,12 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                                       : outi + (size_t)ty0 * Wout * NF);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const bool rok = ty0 + row0 + r < Hout;   // wave-uniform
+                const bool rok = FULL || ty0 + row0 + r < Hout;   // wave-uniform
                 const uint32_t so = (uint32_t)((row0 + r) * Wout) * (OUT_CB ? 64u : 256u);
 #pragma unroll
                 for (int ph = 0; ph < 2; ph++) {
                     const int x = tx0 + 16 * ph + j;
-                    const bool xok = x < Wout;
+                    const bool xok = FULL || x < Wout;
                     const floatx4 &c = acc[(r * 2 + ph) * 4 + q];
                     float o4[4];
                     // OSPL: the outputs scaled by 2^sigma straight from the accumulators (scale folded into
@@ -544,13 +552,17 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                             xp_st4(o, rs, xok ? (uint32_t)(OUT_CB ? x * 64 + 16 * k4 : x * 256 + 64 * q + 16 * k4) : XP_OOB, so);
                         }
                     }
-                    if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
+                    asm volatile("s_nop 2" ::"v"(pin[k >= XP_PIN - 1 ? k - (XP_PIN - 1) : k]) : "memory");   // after each store: >= 9 wait states over XP_PIN stores
                 }
             }
+            if (q == 1) mid();   // half the accumulators stored
         }
 #pragma unroll
         for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
-        asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+        asm volatile("s_nop 7\n\ts_nop 1" ::"v"(pin[NPIN - 1]) : "memory");
+        };
+        if (ty0 + XP_TY <= Hout && tx0 + XP_TX <= Wout) body(std::true_type{});
+        else body(std::false_type{});
         if (OSPL) amax = __float_as_uint(__uint_as_float(amax) / oscale);   // exact: a power of two
         // one atomic per wave and image (flushed when the tiles move to the next image and at the end)
         if (img != amax_img) {
@@ -562,9 +574,11 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
         // a pixel's 64 channels: 4 quarters x 4 lanes (k4) x 4 registers of this wave
         const size_t pix0 = (size_t)img * bt.pix_stride + (size_t)ty0 * Wout;
         const __amdgpu_buffer_rsrc_t rs = xp_rsrc(out + pix0 * NF);
+        auto body = [&](auto fullc) {   // FULL: as above
+        constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const bool rok = ty0 + row0 + r < Hout;
+            const bool rok = FULL || ty0 + row0 + r < Hout;
             const uint32_t so = (uint32_t)((row0 + r) * Wout) * 256u;
 #pragma unroll
             for (int ph = 0; ph < 2; ph++) {
@@ -587,7 +601,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                 ss += __shfl_xor(ss, 16, 64);
                 ss += __shfl_xor(ss, 32, 64);
                 const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
-                const bool xok = x < Wout;
+                const bool xok = FULL || x < Wout;
                 const uint32_t vo = xok ? (uint32_t)(x * 256 + 16 * k4) : XP_OOB;
                 float s2 = 0.0f;
 #pragma unroll
@@ -596,7 +610,7 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                     const int k = (r * 2 + ph) * 4 + q;
                     pin[k] = __builtin_bit_cast(u32x4, o);
                     if (rok) xp_st4(o, rs, vo + 64u * q, so);
-                    if (k >= XP_PIN - 1) asm volatile("" ::"v"(pin[k - (XP_PIN - 1)]));
+                    asm volatile("s_nop 2" ::"v"(pin[k >= XP_PIN - 1 ? k - (XP_PIN - 1) : k]) : "memory");   // after each store: >= 9 wait states over XP_PIN stores
                     if (SPLIT) {   // bf16 split planes of the features (sde_cv_wta_split's input)
                         const float xs[4] = {o.x, o.y, o.z, o.w};
                         bf16x4 hv, lv;
@@ -625,10 +639,14 @@ __device__ __forceinline__ void h16_epilogue(const floatx4 (&acc)[32], int lane,
                     }
                 }
             }
+            if (r == 1) mid();   // half the accumulators stored
         }
 #pragma unroll
         for (int k = NPIN - (XP_PIN - 1); k + 1 < NPIN; k++) asm volatile("" ::"v"(pin[k]));
-        asm volatile("s_nop 4" ::"v"(pin[NPIN - 1]));
+        asm volatile("s_nop 7\n\ts_nop 1" ::"v"(pin[NPIN - 1]) : "memory");
+        };
+        if (ty0 + XP_TY <= Hout && tx0 + XP_TX <= Wout) body(std::true_type{});
+        else body(std::false_type{});
     }
 }
 
@@ -673,7 +691,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
     // c-blocks feeding each B fragment to all four quarters (h16_cblock12), except the last layer with
     // split outputs (its epilogue would spill 13 VGPRs with the 2-tap A ring)
     constexpr bool B12 = H16_B12 == 2 ? !(LAST && SPLIT) : H16_B12 == 1 ? !LAST && !FIRST : false;
-    constexpr int BRD = (IN_CB && OUT_CB && !FIRST && !LAST && !ISPL && !OSPL) ? 3 : 2;
+    constexpr int BRD = 3;
     H16A abuf[4];   // h16_cblock: slots 0-2
     abuf[0] = h16_afrag(ra, avoff, 0, 0);
     abuf[1] = h16_afrag(ra, avoff, 0, 1);
@@ -694,7 +712,7 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
         auto cstep = [&](int cb) {
             if constexpr (B12) {
                 if (cb == 0) h16_cblock12<0, BRD>(acc, abuf, ra, avoff, 0, 1, hsm + cur * H16_STAGE + bbase);
-                else h16_cblock12<2, BRD>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
+                else h16_cblock12<2, BRD, false>(acc, abuf, ra, avoff, 1, 0, hsm + cur * H16_STAGE + bbase);
             } else {
                 h16_cblock(acc, abuf, ra, avoff, cb, cb ^ 1, hsm + cur * H16_STAGE + bbase);
             }
@@ -710,8 +728,15 @@ __global__ __launch_bounds__(512) void conv64_h16_kernel(const float *__restrict
                     if (OSPL) sc_o = xp_out_scale(FIRST, am, hdr);
                     sc_img = img;
                 }
+                // B12: the next tile's first tap (c-block 0, phase 0: slots 0, 1), requested halfway through
+                auto mid = [&]() {
+                    if constexpr (B12) {
+                        abuf[0] = h16_afrag(ra, avoff, 0, 0);
+                        abuf[1] = h16_afrag(ra, avoff, 0, 1);
+                    }
+                };
                 h16_epilogue<LAST, OUT_CB, SPLIT, OSPL>(acc, lane, g, img, ty0, tx0, sc_u, lbias4, out, Hout, Wout, bt, ohi,
-                                                       olo, onrm, amax_run, amax_img, out_amax, sc_o);
+                                                       olo, onrm, amax_run, amax_img, out_amax, sc_o, mid);
             }
             __syncthreads();
             cur ^= 1;

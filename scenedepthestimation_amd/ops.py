@@ -150,8 +150,9 @@ def cv_wta_split(fl, fr, split_l, split_r, d0: int, d1: int, disp=None, min_cost
 
 
 def cv_wta_fixups(workspace) -> int:
-    """Number of pixels the last certified cv_wta call resolved with the exact scan (synchronises)."""
-    return int(workspace[:4].view(torch.int32).item())
+    """Number of pixels the last certified cv_wta call resolved with the exact scan (synchronises): the sum of
+    the workspace's 64 counter words (one per 256-disparity chunk on the chunked path, word 0 otherwise)."""
+    return int(workspace[:256].view(torch.int32).sum().item())
 
 
 def wta(vol, layout: str = "DHW", rule: str = "inf", out=None):

@@ -297,6 +297,11 @@ def test_config5_4k_d512_shards_and_band_tower(gpu, oracle):
     m.features()
     m.cost_wta()
     ref_disp = m.disp.clone()
+    # D = 512 runs the certified row sweep in two 256-disparity chunks; pixels left of a chunk's d0 are resolved
+    # without the exact scan, so the fix-ups stay near-ties only (<= 0.2 % of pixels)
+    nfix = ops.cv_wta_fixups(m.cv_ws)
+    print("C5 certified fix-up pixels:", nfix, "of", H * W)
+    assert nfix <= 0.002 * H * W
     # the sharded tower: 8 row bands with all-reduced (emulated) bound words
     assert torch.equal(_band_features(m, N, "f16x3"), m.feat2)
     torch.cuda.empty_cache()
