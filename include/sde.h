@@ -80,8 +80,9 @@ int sde_wta(const float *vol, int H, int W, int D, int layout, int rule, float *
 
 /* sde_cv_wta modes: both give identical (bit-exact) outputs. */
 #define SDE_CV_EXACT 0       /* every voxel in NumPy's pairwise order on VALU                                */
-#define SDE_CV_CERTIFIED 1   /* bf16x3 MFMA scores + rigorous error bound; pixels whose winner is not
-                                certified by a 2*eps gap are resolved by the exact scan (needs workspace) */
+#define SDE_CV_CERTIFIED 1   /* f16x3 (row sweep) or bf16x3 MFMA scores + rigorous error bound; pixels whose
+                                winner is not certified by a 2*eps gap are resolved by the exact scan
+                                (needs workspace) */
 
 /* Workspace bytes sde_cv_wta needs in SDE_CV_CERTIFIED mode (work-list of unresolved pixels). */
 int64_t sde_cv_wta_workspace_bytes(int H, int W);
@@ -94,8 +95,9 @@ int64_t sde_cv_wta_workspace_bytes(int H, int W);
  * cost, bit-exact) and argmin (int32, -1 if none), [H][W].  Shards merge
  * bit-exactly with sde_argmin_merge (ties -> lower d).  mode: SDE_CV_EXACT or
  * SDE_CV_CERTIFIED (C == 64; other C always run exact).  The workspace's first
- * 4 bytes hold, after the call, the number of pixels the certified mode
- * resolved exactly.
+ * 256 bytes hold, after the call, 64 uint32 counters whose sum is the number of
+ * pixels the certified mode resolved exactly (one per 256-disparity chunk when
+ * d1 - d0 exceeds the row sweep's window, e.g. D = 512; word 0 otherwise).
  */
 int sde_cv_wta(const float *fl, const float *fr, int H, int W, int C, int d0, int d1, float *disp,
                float *min_cost, int32_t *argmin, int mode, void *workspace, int64_t workspace_bytes,
