@@ -462,7 +462,11 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
         float nl = 0.0f;
         unsigned nmax2 = 0u, wbad = 0u;
         bool lbad = false;
-        if (xb < W) {          // wave-uniform
+        if (xb < W && xb + RW_T - 1 < d0) {
+            // every pixel of the group is left of d0: no voxel of the band is in the image (the chunked path's
+            // later chunks, disparity shards past the first); the certificate's `none` case writes (-0.0, d0)
+            if (more) load_left(k + 1);
+        } else if (xb < W) {   // wave-uniform
             rw_f16x8 bh[4], bl[4];
             float ssl = 0.0f;
 #if CV_FASTSPLIT & 1
