@@ -178,6 +178,11 @@ int sde_set_persistent_grid(int cus);
 /* Number of floats of the packed (device-layout) weight blob (fp32 + pre-split bf16 planes). */
 int64_t sde_tower_packed_floats(int nlayers, int nf);
 
+/* 1 if this build's sde_tower_forward* pass split activations (SDE_TOWER_OUT_SPLIT / IN_SPLIT layouts) between
+ * the default f16x3 tower's 64 -> 64 layers, 0 if they pass c-block-major fp32 (the default build).  Layer-by-layer
+ * drivers that must reproduce the forward's bits (the row-band tower of the multi-GPU schemes) follow it. */
+int sde_tower_split_act(void);
+
 /*
  * HOST helper: pack TF HWIO weights ([3][3][Cin][nf], `conv{k}/weights:0`) and
  * biases ([nf], `conv{k}/biases:0`) of nlayers layers into `packed` (host memory,

@@ -50,6 +50,7 @@ SIGNATURES = {
                                                  c_int64, c_void_p]),
     "sde_argmin_merge": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "sde_tower_packed_floats": (c_int64, [c_int, c_int]),
+    "sde_tower_split_act": (c_int, []),
     "sde_tower_pack_weights": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int,
                                        c_void_p]),
     "sde_tower_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),

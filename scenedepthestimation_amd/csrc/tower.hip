@@ -1777,12 +1777,19 @@ static constexpr int64_t SPLIT_MAX_PIX = (int64_t)1 << 24;
 static bool split_ok(int nlayers, int64_t pix) { return nlayers <= XP_SCALE_WORD && pix < SPLIT_MAX_PIX; }
 // the kernels that exist: layer 2 may write split planes; a middle layer reads them iff it writes them; the
 // last layer may read them
-static bool split_pairing_ok(bool in_sp, bool out_sp, int layer, int nlayers, int64_t pix)
+// the pixel limit applies to the split plane itself: the input plane for IN_SPLIT, the output plane (what the
+// forward checks for layer 2's split outputs, h2 * w2) for OUT_SPLIT
+static bool split_pairing_ok(bool in_sp, bool out_sp, int layer, int nlayers, int Hin, int Win)
 {
     if (!in_sp && !out_sp) return true;
-    if (!split_ok(nlayers, pix) || (in_sp && layer == 2) || (out_sp && layer == nlayers)) return false;
+    const int sh = layer == 2 ? 4 : 2;
+    if ((in_sp && !split_ok(nlayers, (int64_t)Hin * Win)) || (out_sp && !split_ok(nlayers, (int64_t)(Hin - sh) * (Win - sh))))
+        return false;
+    if ((in_sp && layer == 2) || (out_sp && layer == nlayers)) return false;
     return layer == 2 || layer == nlayers || in_sp == out_sp;
 }
+
+SDE_EXPORT int sde_tower_split_act(void) { return SDE_SPLIT_ACT; }
 
 static bool tower_flags_ok(int flags, bool layer_api)
 {
@@ -1816,7 +1823,7 @@ SDE_EXPORT int sde_tower_layer_scaled(const float *in, int Hin, int Win, const f
     if ((feat_hi != nullptr) != (feat_lo != nullptr)) return SDE_ERR_ARG;
     if ((flags & SDE_TOWER_F16X3) && (!in_absmax || (layer < nlayers && !out_absmax))) return SDE_ERR_ARG;
     const bool in_sp = (flags & SDE_TOWER_IN_SPLIT) != 0, out_sp = (flags & SDE_TOWER_OUT_SPLIT) != 0;
-    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, (int64_t)Hin * Win)) return SDE_ERR_ARG;
+    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, Hin, Win)) return SDE_ERR_ARG;
     launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, feat_hi, feat_lo, feat_norm, in_cb, out_cb,
                  in_absmax, out_absmax, as_stream(stream), 1, 0, 0, 0, in_sp, out_sp);
     return launch_status();
@@ -1841,7 +1848,7 @@ SDE_EXPORT int sde_tower_layer_batch(const float *in, int nimg, int64_t in_strid
     const bool in_sp = (flags & SDE_TOWER_IN_SPLIT) != 0, out_sp = (flags & SDE_TOWER_OUT_SPLIT) != 0;
     // split activations: a layer's scale word sits 32 words past its bound word, which is column <= 31 of the
     // image's row; rows of fewer than 64 words would put image i's scale word on image i + 1's bound words
-    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, (int64_t)Hin * Win) ||
+    if (!split_pairing_ok(in_sp, out_sp, layer, nlayers, Hin, Win) ||
         ((in_sp || out_sp) && nimg > 1 && amax_stride < (int)(TOWER_AMAX_BYTES / sizeof(float))))
         return SDE_ERR_ARG;
     launch_layer(in, Hin, Win, packed, nlayers, layer, out, flags, nullptr, nullptr, nullptr, in_cb, out_cb,

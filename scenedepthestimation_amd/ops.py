@@ -331,9 +331,10 @@ def absmax_batch(x, out):
 
 SCALE_WORD = 32   # split activations: 2^sigma at bound word + 32 (sde.h SDE_TOWER_OUT_SPLIT)
 AMAX_ROW_WORDS = 64   # a batch's bound-word row per image (tower.hip TOWER_AMAX_BYTES / 4)
-# whether sde_tower_forward* pass split activations between the default f16x3 tower's 64->64 layers
-# (tower.hip SDE_SPLIT_ACT; the layer-by-layer drivers in pipeline.py follow it to stay bit-identical)
-TOWER_SPLIT_ACT = False
+# whether sde_tower_forward* pass split activations between the default f16x3 tower's 64->64 layers, as built
+# (sde_tower_split_act(), tower.hip SDE_SPLIT_ACT; the layer-by-layer drivers in pipeline.py follow it to stay
+# bit-identical)
+TOWER_SPLIT_ACT = bool(lib.sde_tower_split_act())
 
 
 def _layout_flags(flags, in_cblock, out_cblock, in_split, out_split):

@@ -26,7 +26,7 @@ AMAX_WORDS = 64   # f16x3 bound words per image in the tower workspace (TOWER_AM
 SPLIT_MAX_PIX = 1 << 24   # split activations: fewer input pixels per plane than this (tower.hip SPLIT_MAX_PIX)
 # Placement draws of the four SGM volumes (StereoMatcher._place_sgm_volumes): volumes of [MIN, MAX] voxels are
 # placed by up to this many allocate-and-time draws (larger ones would hold three 4-volume sets of > 6 GB each).
-SGM_PLACEMENT_TRIALS = 8
+SGM_PLACEMENT_TRIALS = 16   # round 6: 8 draws missed the fast mode on some boxes (7 slow draws seen in a row)
 SGM_PLACEMENT_MIN_VOXELS = 1 << 26
 SGM_PLACEMENT_MAX_VOXELS = 1 << 29
 

@@ -145,6 +145,14 @@ def test_argument_validation_without_gpu():
                                                      8 | 64 | 128, 1, 1, stride, N)
     for stride in (33, 34, 35, 63):
         assert batch(stride) == ERR, stride
+    # the split pixel limit is on the split plane: layer 2 writes a 4094 x 4092 plane (< 2^24) from a 4098 x 4096
+    # image (> 2^24) -- accepted by the checks (no GPU here: the launch itself fails); a 4098 x 4096 split INPUT
+    # plane is refused
+    big = lambda layer, flags, h, w: lib.sde_tower_layer_scaled(1, h, w, 1, 5, 64, layer, 1, flags, N, N, N, 1, 1, N)
+    assert big(2, 8 | 128, 4098, 4096) not in (ERR, 0)
+    assert big(3, 8 | 64 | 128, 4098, 4096) == ERR
+    from scenedepthestimation_amd import ops
+    assert lib.sde_tower_split_act() in (0, 1) and ops.TOWER_SPLIT_ACT == bool(lib.sde_tower_split_act())
     assert lib.sde_absmax_f32(N, 4, 1, N) == ERR
     assert lib.sde_feature_split(1, 10, 32, 1, 1, 1, N) == ERR                                     # C != 64
     assert lib.sde_cv_wta_split(1, 1, 1, 1, 1, 1, 1, 1, 4, 4, 0, 4, 1, N, N, 1, 0, N) == -3        # workspace
