@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SDE_ABI_VERSION 3
+#define SDE_ABI_VERSION 4
 
 typedef enum {
     SDE_OK = 0,

@@ -21,7 +21,7 @@ c_int, c_int64, c_float, c_double, c_void_p = ctypes.c_int, ctypes.c_int64, ctyp
 c_char_p = ctypes.c_char_p
 
 SDE_OK = 0
-SDE_ABI_VERSION = 3          # include/sde.h: the signatures below are this version's
+SDE_ABI_VERSION = 4          # include/sde.h: the signatures below are this version's
 SDE_LAYOUT_DHW, SDE_LAYOUT_HWD = 0, 1
 SDE_WTA_INIT_INF, SDE_WTA_INIT_D0 = 0, 1
 SDE_SIDE_LEFT, SDE_SIDE_RIGHT = 1, 2

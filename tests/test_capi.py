@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_status_strings():
-    assert _lib.lib.sde_abi_version() == 3 == _lib.SDE_ABI_VERSION
+    assert _lib.lib.sde_abi_version() == 4 == _lib.SDE_ABI_VERSION
     # the header's version is the binding's
     import re
     with open(_lib.os.path.join(_lib.INCLUDE, "sde.h")) as fh:

@@ -87,3 +87,12 @@ s = rep(s, '''    if (!LAST) xp_flush_amax(amax_run, amax_img, lane, out_amax, b
 os.makedirs(os.path.join(ROOT, "tools", "_var"), exist_ok=True)
 open(os.path.join(ROOT, "tools", "_var", "tower_h16_phase.h"), "w").write(s)
 print("wrote tools/_var/tower_h16_phase.h")
+# variant: the stagers skip their loads and splits (barriers only) -- how much of the MFMA waves' loop excess is
+# the stagers' issue on the shared SIMDs
+s2 = rep(s, """        const uint64_t t0 = h16_stamp();
+        if (2 * i + 2 < nh) store(ra, 2 * i + 2);
+        if (2 * i + 4 < nh) load(ra, 2 * i + 4);
+        if (2 * i + 3 < nh) store(rb, 2 * i + 3);
+        if (2 * i + 5 < nh) load(rb, 2 * i + 5);""", """        const uint64_t t0 = h16_stamp();""")
+open(os.path.join(ROOT, "tools", "_var", "tower_h16_phase_nostage.h"), "w").write(s2)
+print("wrote tools/_var/tower_h16_phase_nostage.h")
