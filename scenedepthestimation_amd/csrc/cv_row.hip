@@ -329,10 +329,14 @@ __global__ __launch_bounds__(512) void cv_wta_row_kernel(const float *__restrict
 // ---------------------------------------------------------------------------
 constexpr int R2_NX = 128;                 // left pixels per superstrip (4 compute waves x 32)
 #ifndef CV_FASTSPLIT
-#define CV_FASTSPLIT 31                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle,
-                                           // 16 the stagers' flag from the pixel norm (A/B builds)
+#define CV_FASTSPLIT 63                    // bits: 1 paired split, 2 norm-based flag, 4 swap merges, 8 norm total by shuffle,
+                                           // 16 the stagers' flag from the pixel norm, 32 the stagers' paired split
+                                           // (A/B builds)
 #endif
 constexpr int R2_NEW = R2_NX / RW_T;       // tiles admitted per superstrip (4)
+#ifndef CV_LEAD
+#define CV_LEAD 2                          // scores issued before the next tile's first MFMA (A/B builds: 2..8)
+#endif
 
 // one stager lane's 8 units (pixel u >> 4, channels 4 (u & 15) ..) of right tile T: unit u = lane + 64 i
 __device__ __forceinline__ void r2_load(const float *__restrict__ frrow, int W, int T, int lane, float4 (&v)[8])
@@ -350,13 +354,30 @@ __device__ __forceinline__ void r2_store(uint4 *ring, unsigned *tmax, unsigned *
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const int u = lane + 64 * i, px = u >> 4, q = u & 15;
+        char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
+#if CV_FASTSPLIT & 32
+        // rw_split's parts as the compute waves' left split: hi of a scaled pair by one packed convert, lo by
+        // v_fma_mix{lo,hi} from it (x 2^S - hi exact in fp32: the same bits)
+        const float xs[4] = {v[i].x * RW_SCALE, v[i].y * RW_SCALE, v[i].z * RW_SCALE, v[i].w * RW_SCALE};
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        uint32_t hw[2], lw[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const h2 hh = {(_Float16)xs[2 * e], (_Float16)xs[2 * e + 1]};
+            hw[e] = __builtin_bit_cast(uint32_t, hh);
+            asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lw[e]) : "v"(xs[2 * e]), "v"(hw[e]));
+            asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lw[e]) : "v"(xs[2 * e + 1]), "v"(hw[e]));
+        }
+        *reinterpret_cast<uint2 *>(base) = uint2{hw[0], hw[1]};
+        *reinterpret_cast<uint2 *>(base + 256 * 16) = uint2{lw[0], lw[1]};
+#else
         _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
         rw_split(v[i].x, h0, l0); rw_split(v[i].y, h1, l1); rw_split(v[i].z, h2, l2); rw_split(v[i].w, h3, l3);
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         const h4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
-        char *base = reinterpret_cast<char *>(ring + slot * 512 + fx_slot(px, q >> 1)) + 8 * (q & 1);
         *reinterpret_cast<uint2 *>(base) = __builtin_bit_cast(uint2, hv);
         *reinterpret_cast<uint2 *>(base + 256 * 16) = __builtin_bit_cast(uint2, lv);
+#endif
         // the pixel's squared norm: its 16 lanes are one DPP row (same adds as rw_store)
         float ss = v[i].x * v[i].x + v[i].y * v[i].y + v[i].z * v[i].z + v[i].w * v[i].w;
         ss += rw_dpp<0xB1>(ss);
@@ -595,24 +616,27 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     int dk[4];
 #pragma unroll
                     for (int k2 = 0; k2 < 4; k2++) dk[k2] = dl - 8 * k2;
+                    // CV_LEAD scores before the next tile's first MFMA (they cover its fragments' LDS reads), the
+                    // other 16 - CV_LEAD spread over the 12 MFMA gaps
+                    constexpr int LD = CV_LEAD, RS = 16 - CV_LEAD;
                     if (full) {
                         asm volatile("");
-                        score1(acc, 0, true, dk);
-                        score1(acc, 1, true, dk);
+#pragma unroll
+                        for (int r = 0; r < LD; r++) score1(acc, r, true, dk);
 #pragma unroll
                         for (int m = 0; m < 12; m++) {
                             if (issue) mfma(m, accn, fbh, fbl);
 #pragma unroll
-                            for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, true, dk);
+                            for (int r = LD + (RS * m) / 12; r < LD + (RS * (m + 1)) / 12; r++) score1(acc, r, true, dk);
                         }
                     } else {
-                        score1(acc, 0, false, dk);
-                        score1(acc, 1, false, dk);
+#pragma unroll
+                        for (int r = 0; r < LD; r++) score1(acc, r, false, dk);
 #pragma unroll
                         for (int m = 0; m < 12; m++) {
                             if (issue) mfma(m, accn, fbh, fbl);
 #pragma unroll
-                            for (int r = 2 + (14 * m) / 12; r < 2 + (14 * (m + 1)) / 12; r++) score1(acc, r, false, dk);
+                            for (int r = LD + (RS * m) / 12; r < LD + (RS * (m + 1)) / 12; r++) score1(acc, r, false, dk);
                         }
                     }
                 };
