@@ -837,51 +837,83 @@ __global__ __launch_bounds__(256) void cv_wta_cert_kernel(const float *__restric
 }
 
 
-// Exact resolution of the listed pixels: one wave per pixel, lanes split the
-// d range (increasing d per lane), then a (value, index) merge == sequential scan.
+// Exact resolution of the listed pixels, one 4-wave workgroup per pixel (persistent over the list).
+// Wave v takes disparities [d0 + vQ, d0 + (v+1)Q), Q = 8 ceil(D / 32); each of its 8 lane groups of 8
+// takes one disparity per iteration, lane jj of a group the products of channels 8m + jj, m = 0..7, in
+// order -- dot64_exact_global's partial sum acc[jj] -- and the group's xor butterfly adds the 8 partial
+// sums in that function's tree order (adds are commutative: the same bits).  A group scans its
+// disparities in increasing d with a strict <, then (value, index) merges over the groups and the waves
+// give the sequential first minimum.  All of a wave's iterations are in flight at once up to D = 256 (a
+// chunk): one round of loads per pixel instead of a lane's three to four dependent 16-load dots, whose
+// 64 lanes each read another pixel's 256 B (64 cache lines per load instruction).
+constexpr int FX2_U = 8;   // iterations per round of loads
 __global__ __launch_bounds__(256) void cv_wta_fixup_kernel(const float *__restrict__ fl, const float *__restrict__ fr,
                                                            int W, int d0, int d1, const unsigned *__restrict__ counter,
                                                            const int32_t *__restrict__ list, float *__restrict__ out_min,
                                                            int32_t *__restrict__ out_arg, float *__restrict__ out_disp)
 {
+    __shared__ float wb[4];
+    __shared__ int wa[4];
     const unsigned cnt = *counter;
-    const int lane = threadIdx.x & 63;
-    const unsigned nw = gridDim.x * 4;
-    for (unsigned e = blockIdx.x * 4 + (threadIdx.x >> 6); e < cnt; e += nw) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 3, jj = lane & 7;
+    const int Q = (d1 - d0 + 31) / 32 * 8;
+    const int dw = d0 + wave * Q, dwe = min(d1, dw + Q);
+    for (unsigned e = blockIdx.x; e < cnt; e += gridDim.x) {
         const size_t p = (size_t)list[e];
         const int x = (int)(p % W);
         const size_t rowbase = p - x;
-        const float4 *a = reinterpret_cast<const float4 *>(fl + p * 64);
+        float av[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) av[m] = fl[p * 64 + 8 * m + jj];
         float best = __builtin_inff();
         int arg = -1;
-        // four disparities per lane in flight at once (their row loads overlap), then the
-        // in-order first-min scan over them
-        for (int db = d0 + lane; db < d1; db += 256) {
-            float c4[4];
+        for (int db = dw; db < dwe; db += 8 * FX2_U) {
+            float bv[FX2_U][8];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int d = db + 64 * u;
-                const int xr = x - d;
-                const float cv = dot64_exact_global(a, reinterpret_cast<const float4 *>(fr + (rowbase + (xr >= 0 ? xr : 0)) * 64));
-                c4[u] = (d < d1 && xr >= 0) ? cv : -0.0f;
+            for (int u = 0; u < FX2_U; u++) {
+                const int xr = x - (db + 8 * u + g);
+                const float *b = fr + (rowbase + (xr >= 0 ? xr : 0)) * 64 + jj;
+#pragma unroll
+                for (int m = 0; m < 8; m++) bv[u][m] = b[8 * m];
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int d = db + 64 * u;
-                if (d < d1 && c4[u] < best) { best = c4[u]; arg = d; }
+            for (int u = 0; u < FX2_U; u++) {
+                const int d = db + 8 * u + g;
+                float acc = av[0] * bv[u][0];
+#pragma unroll
+                for (int m = 1; m < 8; m++) acc = acc + av[m] * bv[u][m];
+                acc = acc + __shfl_xor(acc, 1, 64);   // (acc0 + acc1), (acc2 + acc3), ...
+                acc = acc + __shfl_xor(acc, 2, 64);   // ((acc0 + acc1) + (acc2 + acc3)), ...
+                acc = acc + __shfl_xor(acc, 4, 64);
+                const float c = x - d >= 0 ? -(0.0f + acc) : -0.0f;
+                if (d < dwe && c < best) {
+                    best = c;
+                    arg = d;
+                }
             }
         }
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
+        for (int off = 8; off < 64; off <<= 1) {
             const float ob = __shfl_xor(best, off, 64);
             const int oa = __shfl_xor(arg, off, 64);
             argmin_merge(best, arg, ob, oa);
         }
         if (lane == 0) {
+            wb[wave] = best;
+            wa[wave] = arg;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            best = wb[0];
+            arg = wa[0];
+#pragma unroll
+            for (int v = 1; v < 4; v++) argmin_merge(best, arg, wb[v], wa[v]);
             if (out_min) out_min[p] = best;
             if (out_arg) out_arg[p] = arg;
             if (out_disp) out_disp[p] = (float)arg;
         }
+        __syncthreads();
     }
 }
 
