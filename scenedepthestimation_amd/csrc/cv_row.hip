@@ -590,10 +590,17 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                                                                                 acc, 0, 0, 0);
                     else acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m - 8], bh[m - 8], acc, 0, 0, 0);
                 };
-                auto score1 = [&](const fx_floatx16 &acc, int r, bool full, const int (&dk)[4]) {
+                // MODE 0: a full tile (every voxel in [d0, d1)); 1: only d < d1 can fail (d = dk - tt < d1 <=>
+                // dk < d1 + tt: one compare against a per-tt scalar); 3: only d >= d0 can fail (dk >= d0 + tt);
+                // 2: both
+                auto score1 = [&](const fx_floatx16 &acc, int r, auto mode_c, const int (&dk)[4]) {
+                    constexpr int MODE = decltype(mode_c)::value;
                     const int tt = r & 3;
-                    const float sc = full || ((dk[r >> 2] - tt) >= d0 && (dk[r >> 2] - tt) < d1) ? acc[r]
-                                                                                                 : -__builtin_inff();
+                    const bool in = MODE == 0   ? true
+                                    : MODE == 1 ? dk[r >> 2] < d1 + tt
+                                    : MODE == 3 ? dk[r >> 2] >= d0 + tt
+                                                : (dk[r >> 2] - tt) >= d0 && (dk[r >> 2] - tt) < d1;
+                    const float sc = in ? acc[r] : -__builtin_inff();
                     const bool gt = sc > b1[tt];
                     ag[tt] = gt ? dk[r >> 2] : ag[tt];
                     b2[tt] = __builtin_amdgcn_fmed3f(b1[tt], b2[tt], sc);
@@ -611,7 +618,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     nmax2 = max(nmax2, tmax[sl2]);
                     wbad |= tbad[sl2];
                     const int dt = xb - RW_T * T;
-                    const bool full = dt - 31 >= d0 && dt + 31 < d1;      // wave-uniform
+                    const bool lowok = dt - 31 >= d0, highok = dt + 31 < d1;   // wave-uniform
                     const int dl = dt + j - 4 * h;
                     int dk[4];
 #pragma unroll
@@ -619,25 +626,26 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                     // CV_LEAD scores before the next tile's first MFMA (they cover its fragments' LDS reads), the
                     // other 16 - CV_LEAD spread over the 12 MFMA gaps
                     constexpr int LD = CV_LEAD, RS = 16 - CV_LEAD;
-                    if (full) {
+                    auto body = [&](auto mode_c) {
+#pragma unroll
+                        for (int r = 0; r < LD; r++) score1(acc, r, mode_c, dk);
+#pragma unroll
+                        for (int m = 0; m < 12; m++) {
+                            if (issue) mfma(m, accn, fbh, fbl);
+#pragma unroll
+                            for (int r = LD + (RS * m) / 12; r < LD + (RS * (m + 1)) / 12; r++)
+                                score1(acc, r, mode_c, dk);
+                        }
+                    };
+                    if (lowok && highok) {
                         asm volatile("");
-#pragma unroll
-                        for (int r = 0; r < LD; r++) score1(acc, r, true, dk);
-#pragma unroll
-                        for (int m = 0; m < 12; m++) {
-                            if (issue) mfma(m, accn, fbh, fbl);
-#pragma unroll
-                            for (int r = LD + (RS * m) / 12; r < LD + (RS * (m + 1)) / 12; r++) score1(acc, r, true, dk);
-                        }
+                        body(std::integral_constant<int, 0>{});
+                    } else if (!WANT_MIN && lowok) {   // (WANT_MIN: the two extra bodies spill there)
+                        body(std::integral_constant<int, 1>{});
+                    } else if (!WANT_MIN && highok) {
+                        body(std::integral_constant<int, 3>{});
                     } else {
-#pragma unroll
-                        for (int r = 0; r < LD; r++) score1(acc, r, false, dk);
-#pragma unroll
-                        for (int m = 0; m < 12; m++) {
-                            if (issue) mfma(m, accn, fbh, fbl);
-#pragma unroll
-                            for (int r = LD + (RS * m) / 12; r < LD + (RS * (m + 1)) / 12; r++) score1(acc, r, false, dk);
-                        }
+                        body(std::integral_constant<int, 2>{});
                     }
                 };
                 if (n > 0) {
