@@ -479,6 +479,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
         const int x = xb + j;
         const bool xok = x < W;
         float best = -__builtin_inff(), second = -__builtin_inff();
+        float wcost = -0.0f;   // WANT_MIN: the winner's exact cost (computed before the barrier)
         int arg = -1;
         float nl = 0.0f;
         unsigned nmax2 = 0u, wbad = 0u;
@@ -696,6 +697,36 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
 #endif
                 fx_merge(best, arg, second, bb, aa, ss2);
             }
+            if constexpr (WANT_MIN) {
+                // the winner's exact cost (used if the pixel certifies), by both lane halves and issued before the
+                // barrier: lane (j, h) forms dot64_exact_global's partial sums acc[4h .. 4h+3] (channels 8m + 4h ..
+                // 8m + 4h + 3 = float4 2m + h of each operand, all 16 loads in flight) and its half of the final tree,
+                // ((acc0 + acc1) + (acc2 + acc3)) or ((acc4 + acc5) + (acc6 + acc7)); a permlane32 swap adds the
+                // halves in that order: the same bits, one round of loads instead of dot64_exact_global_lean's eight
+                const uint32_t lo_arg = __builtin_amdgcn_permlane32_swap((uint32_t)arg, (uint32_t)arg, false, false)[0];
+                const int ab = h ? (int)lo_arg : arg;   // the upper half takes lane j's merged arg
+                const int xr = x - ab;
+                const bool ok = xok && ab >= 0 && xr >= 0;
+                const float4 *la = reinterpret_cast<const float4 *>(flrow + (size_t)(xok ? x : 0) * 64) + h;
+                const float4 *ra = reinterpret_cast<const float4 *>(frrow + (size_t)(ok ? xr : 0) * 64) + h;
+                float4 lv[8], rv[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    lv[m] = la[2 * m];
+                    rv[m] = ra[2 * m];
+                }
+                float a4[4];
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    const float p4[4] = {lv[m].x * rv[m].x, lv[m].y * rv[m].y, lv[m].z * rv[m].z, lv[m].w * rv[m].w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) a4[e] = m == 0 ? p4[e] : a4[e] + p4[e];
+                }
+                const float half = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+                const float other = __uint_as_float(
+                    __builtin_amdgcn_permlane32_swap(__float_as_uint(half), __float_as_uint(half), false, false)[1]);
+                wcost = -(0.0f + (half + other));   // lanes 0-31: (lower half) + (upper half)
+            }
         }
         // window k+1's new tiles go into the slots superstrip k-1 read (not this window's): one
         // barrier per superstrip orders both directions
@@ -713,9 +744,7 @@ __global__ __launch_bounds__(512) void cv_wta_row2_kernel(const float *__restric
                 if (none) arg = d0;
                 if (WANT_MIN) {
                     float cost = -0.0f;
-                    if (x - arg >= 0)
-                        cost = dot64_exact_global_lean(reinterpret_cast<const float4 *>(flrow + (size_t)x * 64),
-                                                  reinterpret_cast<const float4 *>(frrow + (size_t)(x - arg) * 64));
+                    if (x - arg >= 0) cost = wcost;
                     out_min[p] = cost;
                 }
                 if (out_arg) out_arg[p] = arg;
